@@ -1,0 +1,170 @@
+"""Benchmark: rays/s of the hierarchical render path at 800x800, 64 coarse + 128 fine samples.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = render one 800x800 frame (640,000 rays) per GPU: get_rays -> render_rays
+(hierarchical H1: coarse 64, inverse-CDF 128, fine pass over the 192 merged samples) with
+in-kernel stratified / inverse-CDF RNG, on a random-init NeRF of the reference architecture
+(torch.manual_seed(0); NeRF(Config())).  With N > 1 GPUs each rank renders its own frame of
+the run.py circle path (rank r = frame r: weak scaling, 640,000 rays per GPU) and the
+frames are reassembled on every rank with one RCCL all-gather of [r,g,b,depth] per ray.
+Rank 0 prints one JSON line.  value = rays of all ranks / max-over-ranks wall time.
+
+roofline: the dominant kernel is the fused PE->MLP kernel (mlp_kernel).  Its algorithmic
+work is 1,048,832 FLOP per evaluated sample; each step launches it
+twice (B*64 and B*192 samples).  achieved = algorithmic FLOP / kernel time, the time
+measured with HIP events around every launch inside the timed steps (on the stream it runs
+on); peak = the fp32 MFMA dense peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+cpu_baseline: the oracle (PyTorch-CPU restatement, oracle/nerf_oracle.py) timed on a
+bounded sample of the same workload on this host's cores (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+H = W = 800
+N_COARSE, N_FINE = 64, 128
+FLOP_PER_SAMPLE = 1_048_832           # SURVEY.md §8d, DESIGN.md §Roofline
+MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scene", default="chair")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
+    return p.parse_args()
+
+
+def cpu_baseline(target_s):
+    """Oracle H1 render of a centre block of the same frame on the host cores."""
+    from oracle import nerf_oracle as O
+    from nerfmi import cameras
+    state = O.random_state(0)
+    torch.manual_seed(1)
+    app = torch.randn(100, 32)[0]
+    o, d = O.get_rays(H, W, cameras.synthetic_focal(W), cameras.frame_c2w("chair"))
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    centre = (H // 2) * W + W // 2
+
+    def run(n):
+        sl = slice(centre - n // 2, centre - n // 2 + n)
+        torch.manual_seed(2)
+        t_rand = torch.rand(n, N_COARSE)
+        u_rand = torch.rand(n, N_FINE)
+        t0 = time.perf_counter()
+        O.render_rays_h1(state, o[sl].contiguous(), d[sl].contiguous(), 2.0, 6.0, N_COARSE, N_FINE, app,
+                         t_rand, u_rand)
+        return time.perf_counter() - t0
+
+    n = 512
+    dt = run(n)
+    n = int(min(65536, max(n, n * target_s / max(dt, 1e-3))))
+    n = max(512, (n // 512) * 512)
+    dt = run(n)
+    return {"value": n / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} contiguous rays at the centre of the 800x800 chair frame 0, hierarchical "
+                      f"{N_COARSE}+{N_FINE} (H1), perturbed, oracle/nerf_oracle.py on PyTorch-CPU fp32, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import nerfmi
+    from nerfmi import cameras
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.manual_seed(0)
+    model = nerfmi.NeRF(nerfmi.Config()).to(dev).eval()
+    torch.manual_seed(1)
+    app = torch.randn(100, 32)[0].to(dev)
+    focal = cameras.synthetic_focal(W)
+    c2w = cameras.frame_c2w(args.scene, "circle", frame=rank % 120, num_frames=120).to(dev)
+    B = H * W
+    frames = torch.empty(world, B, 4, device=dev) if world > 1 else None
+
+    def step(i, timing=None):
+        o, d = nerfmi.get_rays(H, W, focal, c2w)
+        rgb, depth, _ = nerfmi.render_rays(model, o.reshape(-1, 3), d.reshape(-1, 3), 2.0, 6.0, N_COARSE, N_FINE,
+                                           appearance_embedding=app, perturb=True, hierarchical=True,
+                                           seed=1000 * rank + i, timing=timing)
+        if world > 1:
+            dist.all_gather_into_tensor(frames.view(-1), torch.cat([rgb, depth], dim=1).reshape(-1))
+        return rgb
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timing = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, timing)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in timing)
+    mlp_samples = sum(n for _, _, n in timing)
+    achieved = mlp_samples * FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12
+    if rank == 0:
+        total_rays = B * world * args.steps
+        line = {
+            "metric": "rays/sec at 800x800, 64 coarse + 128 fine samples",
+            "value": total_rays / elapsed,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: run.py circle-path pose per rank, random-init NeRF (torch.manual_seed(0)), "
+                    "no dataset/checkpoint in the environment",
+            "config": {"workload": f"{args.scene} 800x800 frame per GPU, hierarchical {N_COARSE} coarse + "
+                                   f"{N_FINE} fine (H1, fine pass over 192 merged samples), perturb=True",
+                       "rays_per_gpu_per_step": B, "n_coarse": N_COARSE, "n_fine": N_FINE,
+                       "parallelism": f"ray-shard x{world} (one frame per GPU) + RCCL all-gather"},
+            "roofline": {"bound": "mfma", "kernel": "mlp_kernel", "achieved": achieved,
+                         "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS,
+                         "traffic": None, "launches": len(timing),
+                         "avg_launch_ms": mlp_ms / max(len(timing), 1),
+                         "flop_per_sample": FLOP_PER_SAMPLE},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""ctypes binding of libnerfmi.so (include/nerfmi.h) — the only way nerfmi computes.
+
+There is deliberately no CPU fallback: if the library is missing, or no HIP device is
+visible, every compute entry point raises RuntimeError.  PyTorch supplies device memory
+and the current HIP stream; all arithmetic happens in the library's HIP kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG_DIR, "libnerfmi.so")
+
+_c_float_p = ctypes.c_void_p  # device pointers travel as integers
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "nerf_last_error": (ctypes.c_char_p, []),
+    "nerf_abi_version": (ctypes.c_int, []),
+    "nerf_get_rays": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.POINTER(ctypes.c_float),
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_normalize_dirs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_positional_encoding": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_sample_stratified": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,
+                                              ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
+    "nerf_sample_importance": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
+    "nerf_packed_weights_floats": (ctypes.c_size_t, []),
+    "nerf_pack_weights": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_pack_weights_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "nerf_ray_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_composite": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+    "nerf_render_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int, ctypes.c_int]),
+    "nerf_render_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p]),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+def load():
+    """Load libnerfmi.so (import torch first so its HIP runtime is the one the library binds to)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"nerfmi: {LIB_PATH} is missing — build it with "
+                               f"`python -c 'import __graft_entry__ as g; g.build()'` (or make -C {_PKG_DIR})")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().nerf_last_error().decode(errors="replace")
+        raise RuntimeError(f"nerfmi: {what} failed (status {rc}): {msg}")
+
+
+def device():
+    """The HIP device all nerfmi work runs on; raises when there is none (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("nerfmi: no HIP device is visible; the render path runs only on the GPU "
+                           "(there is no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None

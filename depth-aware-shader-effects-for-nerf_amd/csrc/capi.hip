@@ -1,0 +1,244 @@
+// C ABI of libnerfmi.so (include/nerfmi.h): argument checks, the weight packer and the
+// whole-path orchestration.  Kernels live in rays.hip, mlp.hip, composite.hip and
+// importance.hip; this file only validates, carves the workspace and launches them in
+// stream order.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace nerf {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+// ---------------------------------------------------------------------------- packing
+// Value of packed element e (layout.h) from the 24 state_dict tensors.
+NERF_HD inline float pack_value(const float* const* P, size_t e) {
+  if (e < kFragFloats) {
+    int m = 0;
+    while (m + 1 < kNumFragMats && e >= frag_offset(m + 1)) ++m;
+    const size_t rel = e - frag_offset(m);
+    const int j = (int)(rel & 3);
+    const int lane = (int)((rel >> 2) & 63);
+    const size_t blk = rel >> 8;
+    const int ksq = frag_ksteps(m) / 4;
+    const int nt = (int)(blk / ksq), kq = (int)(blk % ksq);
+    const int col = frag_source_col(m, 4 * kq + j, lane);
+    if (col < 0) return 0.0f;
+    const int row = nt * 32 + (lane & 31);
+    if (m == 8) return P[P_DIR_W][(size_t)row * (kHidden + kDirEnc) + col];
+    const int layer = (m == kSkipPeMat) ? kSkipLayer : m;
+    const int K = (layer == 0) ? kPosEnc : (layer == kSkipLayer ? kHidden + kPosEnc : kHidden);
+    return P[2 * layer][(size_t)row * K + col];
+  }
+  if (e < kOffSigmaW) {
+    const size_t k = e - kOffBias;
+    return P[2 * (k / kHidden) + 1][k % kHidden];
+  }
+  if (e < kOffSigmaB) return P[P_SIGMA_W][e - kOffSigmaW];
+  if (e < kOffDirB) return e == kOffSigmaB ? P[P_SIGMA_B][0] : 0.0f;
+  if (e < kOffDirWd) return P[P_DIR_B][e - kOffDirB];
+  if (e < kOffAppW) {
+    const size_t k = e - kOffDirWd;
+    return P[P_DIR_W][(k / kDirEnc) * (kHidden + kDirEnc) + kHidden + k % kDirEnc];
+  }
+  if (e < kOffAppB) return P[P_APP_W][e - kOffAppW];
+  if (e < kOffRgbW) return P[P_APP_B][e - kOffAppB];
+  if (e < kOffRgbB) return P[P_RGB_W][e - kOffRgbW];
+  return (e - kOffRgbB < 3) ? P[P_RGB_B][e - kOffRgbB] : 0.0f;
+}
+
+struct ParamPtrs { const float* p[P_COUNT]; };
+
+__global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restrict__ packed) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < kPackedFloats) packed[e] = pack_value(P.p, e);
+}
+
+int launch_pack(const float* const* params, float* packed, hipStream_t s) {
+  ParamPtrs P;
+  for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kPackedFloats + 255) / 256)), dim3(256), 0, s, P, packed);
+  return check_launch("pack_kernel");
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace nerf
+
+using namespace nerf;
+
+#define REQUIRE(cond, ...)                                   \
+  do {                                                       \
+    if (!(cond)) return set_error(NERF_ERR_BAD_ARG, __VA_ARGS__); \
+  } while (0)
+
+extern "C" {
+
+const char* nerf_last_error(void) { return g_err; }
+int nerf_abi_version(void) { return 1; }
+
+int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
+                  float* rays_d, nerf_stream_t stream) {
+  REQUIRE(H > 0 && W > 0, "nerf_get_rays: H=%d W=%d must be positive", H, W);
+  REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= H, "nerf_get_rays: rows [%d,%d) outside [0,%d)", row0,
+          row0 + nrows, H);
+  REQUIRE(c2w_host && rays_d, "nerf_get_rays: null pointer");
+  return launch_get_rays(H, W, focal, c2w_host, row0, nrows, rays_o, rays_d, (hipStream_t)stream);
+}
+
+int nerf_normalize_dirs(const float* rays_d, int64_t B, float* out, nerf_stream_t stream) {
+  REQUIRE(B >= 0, "nerf_normalize_dirs: B=%lld", (long long)B);
+  REQUIRE(B == 0 || (rays_d && out), "nerf_normalize_dirs: null pointer");
+  return launch_normalize(rays_d, B, out, (hipStream_t)stream);
+}
+
+int nerf_positional_encoding(const float* x, int64_t M, int dims, int levels, int include_input, float* out,
+                             nerf_stream_t stream) {
+  REQUIRE(M >= 0 && dims >= 1 && levels >= 0 && levels <= 30, "nerf_positional_encoding: M=%lld dims=%d levels=%d",
+          (long long)M, dims, levels);
+  REQUIRE(M == 0 || (x && out), "nerf_positional_encoding: null pointer");
+  return launch_pe(x, M, dims, levels, include_input, out, (hipStream_t)stream);
+}
+
+int nerf_sample_stratified(const float* rays_o, const float* rays_d, int64_t B, double near, double far, int N,
+                           const float* t_vals, int perturb, const float* t_rand, uint64_t seed, float* z_vals,
+                           float* pts, nerf_stream_t stream) {
+  REQUIRE(B >= 0 && N >= 1, "nerf_sample_stratified: B=%lld N=%d", (long long)B, N);
+  REQUIRE(B == 0 || (t_vals && z_vals), "nerf_sample_stratified: null pointer");
+  REQUIRE(!pts || (rays_o && rays_d), "nerf_sample_stratified: pts requested without rays");
+  return launch_stratified(rays_o, rays_d, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed,
+                           z_vals, pts, (hipStream_t)stream);
+}
+
+int nerf_sample_importance(const float* rays_o, const float* rays_d, const float* z_vals, const float* weights,
+                           int64_t B, int N, int Nf, const float* u_lin, const float* u_rand, uint64_t seed,
+                           float* z_all, float* pts_all, nerf_stream_t stream) {
+  REQUIRE(B >= 0, "nerf_sample_importance: B=%lld", (long long)B);
+  if (N < 1 || N > 256 || Nf < 1 || Nf > 1024)
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_sample_importance: N=%d (1..256) Nf=%d (1..1024)", N, Nf);
+  REQUIRE(B == 0 || (z_vals && weights && u_lin && z_all), "nerf_sample_importance: null pointer");
+  REQUIRE(!pts_all || (rays_o && rays_d), "nerf_sample_importance: pts requested without rays");
+  return launch_importance(rays_o, rays_d, z_vals, weights, B, N, Nf, u_lin, u_rand, seed, z_all, pts_all,
+                           (hipStream_t)stream);
+}
+
+size_t nerf_packed_weights_floats(void) { return kPackedFloats; }
+
+int nerf_pack_weights(const float* const* params, float* packed, nerf_stream_t stream) {
+  REQUIRE(params && packed, "nerf_pack_weights: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) REQUIRE(params[i], "nerf_pack_weights: parameter %d is null", i);
+  return launch_pack(params, packed, (hipStream_t)stream);
+}
+
+int nerf_pack_weights_host(const float* const* params, float* packed) {
+  REQUIRE(params && packed, "nerf_pack_weights_host: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) REQUIRE(params[i], "nerf_pack_weights_host: parameter %d is null", i);
+  for (size_t e = 0; e < kPackedFloats; ++e) packed[e] = pack_value(params, e);
+  return NERF_OK;
+}
+
+int nerf_ray_features(const float* packed, const float* dirs, int64_t R, const float* app, int64_t app_rows,
+                      float* feat, nerf_stream_t stream) {
+  REQUIRE(R >= 0, "nerf_ray_features: R=%lld", (long long)R);
+  REQUIRE(app_rows == 0 || app_rows == 1 || app_rows == R, "nerf_ray_features: app_rows=%lld with R=%lld",
+          (long long)app_rows, (long long)R);
+  REQUIRE(R == 0 || (packed && dirs && feat && (app_rows == 0 || app)), "nerf_ray_features: null pointer");
+  return launch_ray_features(packed, dirs, R, app, app_rows, feat, (hipStream_t)stream);
+}
+
+int nerf_mlp_forward(const float* packed, const float* origins, const float* dirs, const float* z_vals, int64_t R,
+                     int N, const float* ray_feat, float* rgb, float* sigma, nerf_stream_t stream) {
+  REQUIRE(R >= 0 && N >= 1, "nerf_mlp_forward: R=%lld N=%d", (long long)R, N);
+  REQUIRE(z_vals || N == 1, "nerf_mlp_forward: without z_vals the origins are the points and N must be 1");
+  REQUIRE(R == 0 || (packed && origins && ray_feat && rgb && sigma && (!z_vals || dirs)),
+          "nerf_mlp_forward: null pointer");
+  return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, (hipStream_t)stream);
+}
+
+int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, int64_t B, int N, float* rgb_map,
+                   float* depth_map, float* weights, nerf_stream_t stream) {
+  REQUIRE(B >= 0, "nerf_composite: B=%lld", (long long)B);
+  if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_composite: N=%d (1..4096)", N);
+  REQUIRE(B == 0 || (rgb && sigma && z_vals && rgb_map && depth_map), "nerf_composite: null pointer");
+  return launch_composite(rgb, sigma, z_vals, B, N, rgb_map, depth_map, weights, (hipStream_t)stream);
+}
+
+// Workspace carve of nerf_render_rays, in this order (each region 256-B aligned):
+//   dirs (B,3) | z (B,N) | feat (B,256) | rgb (B,T,3) | sigma (B,T) | w (B,N) | z_all (B,T) | maps (B,4)
+// with T = N + Nf.
+static size_t carve(int64_t B, int N, int Nf, size_t* off) {
+  const size_t T = (size_t)N + Nf;
+  const size_t sizes[8] = {(size_t)B * 3, (size_t)B * N, (size_t)B * kRayFeat, (size_t)B * T * 3, (size_t)B * T,
+                           (size_t)B * N, (size_t)B * T, (size_t)B * 4};
+  size_t at = 0;
+  for (int i = 0; i < 8; ++i) {
+    off[i] = at;
+    at += align_up(sizes[i] * sizeof(float));
+  }
+  return at;
+}
+
+size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf) {
+  if (B < 0 || N < 1 || Nf < 0) return 0;
+  size_t off[8];
+  return carve(B, N, Nf, off);
+}
+
+int nerf_render_rays(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
+                     double far, int N, int Nf, const float* t_vals, const float* u_lin, int perturb,
+                     const float* t_rand, const float* u_rand, uint64_t seed, const float* app, int64_t app_rows,
+                     float* rgb_map, float* depth_map, float* weights_out, float* z_out, float* coarse_rgb,
+                     float* coarse_depth, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
+  REQUIRE(B >= 0, "nerf_render_rays: B=%lld", (long long)B);
+  if (N < 1 || N > 4096 || Nf < 0 || N + Nf > 4096 || (Nf > 0 && (N > 256 || Nf > 1024)))
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_render_rays: N=%d Nf=%d outside the supported range", N, Nf);
+  if (B == 0) return NERF_OK;
+  REQUIRE(packed && rays_o && rays_d && t_vals && rgb_map && depth_map && workspace, "nerf_render_rays: null pointer");
+  REQUIRE(Nf == 0 || u_lin, "nerf_render_rays: u_lin required when Nf > 0");
+  REQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_render_rays: app_rows=%lld with B=%lld",
+          (long long)app_rows, (long long)B);
+  REQUIRE(app_rows == 0 || app, "nerf_render_rays: null appearance");
+  size_t off[8];
+  const size_t need = carve(B, N, Nf, off);
+  if (ws_bytes < need)
+    return set_error(NERF_ERR_WORKSPACE, "nerf_render_rays: workspace %zu < %zu bytes", ws_bytes, need);
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  float* dn = (float*)(ws + off[0]);
+  float* z = (Nf == 0 && z_out) ? z_out : (float*)(ws + off[1]);
+  float* feat = (float*)(ws + off[2]);
+  float* rgb = (float*)(ws + off[3]);
+  float* sigma = (float*)(ws + off[4]);
+  float* wc = (Nf == 0) ? weights_out : (float*)(ws + off[5]);
+  float* z_all = z_out ? z_out : (float*)(ws + off[6]);
+  float* maps = (float*)(ws + off[7]);
+  int rc;
+  if ((rc = launch_normalize(rays_d, B, dn, s))) return rc;                                   // render.py:19
+  if ((rc = launch_stratified(rays_o, dn, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed,
+                              z, nullptr, s)))
+    return rc;                                                                                 // render.py:22
+  if ((rc = launch_ray_features(packed, dn, B, app, app_rows, feat, s))) return rc;
+  if ((rc = launch_mlp(packed, rays_o, dn, z, B, N, feat, rgb, sigma, s))) return rc;         // render.py:49
+  if (Nf == 0)
+    return launch_composite(rgb, sigma, z, B, N, rgb_map, depth_map, wc, s);                   // render.py:56-80
+  float* crgb = coarse_rgb ? coarse_rgb : maps;
+  float* cdepth = coarse_depth ? coarse_depth : maps + 3 * B;
+  if ((rc = launch_composite(rgb, sigma, z, B, N, crgb, cdepth, wc, s))) return rc;
+  if ((rc = launch_importance(rays_o, dn, z, wc, B, N, Nf, u_lin, u_rand, seed ^ 0x5DEECE66Dull, z_all, nullptr,
+                              s)))
+    return rc;
+  if ((rc = launch_mlp(packed, rays_o, dn, z_all, B, N + Nf, feat, rgb, sigma, s))) return rc;
+  return launch_composite(rgb, sigma, z_all, B, N + Nf, rgb_map, depth_map, weights_out, s);
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+// Packed-weight layout of the fused MLP (shared by the device pack kernel, the host
+// packer and the MLP kernel).  DESIGN.md §"Weight layout" explains it; in short:
+//
+// The MLP runs every dense layer as out^T = W . in^T on v_mfma_f32_32x32x2_f32 with
+// A = W (32 output neurons x 2 inputs per instruction) and B = the activations
+// (2 inputs x 32 samples).  The 32x32 accumulator of one layer holds, in lane l and
+// register g, sample (l & 31) and neuron (g&3) + 8(g>>2) + 4(l>>5) of a 32-neuron
+// tile.  The next layer consumes that register directly as its B operand (k-step
+// "register g of tile t"), so the k order of every weight matrix is permuted to
+// match, here, once, at pack time.  Positional-encoding inputs use a fixed k order
+// too (pe_feature below).
+//
+// A fragment block is one (n-tile, 4 consecutive k-steps) pair: 64 lanes x 4 floats,
+// lane l holding W[nt*32 + (l&31)][col(ks, l>>5)] for ks = 4*kq .. 4*kq+3, so one
+// wave reads a block with one coalesced 16-byte-per-lane load.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#if defined(__HIPCC__)
+#define NERF_HD __host__ __device__
+#else
+#define NERF_HD
+#endif
+
+namespace nerf {
+
+constexpr int kHidden = 256;
+constexpr int kPosLevels = 10;
+constexpr int kDirLevels = 4;
+constexpr int kPosEnc = 3 * (1 + 2 * kPosLevels);  // 63
+constexpr int kDirEnc = 3 * (1 + 2 * kDirLevels);  // 27
+constexpr int kAppDim = 32;
+constexpr int kDirHidden = kHidden / 2;             // 128
+constexpr int kSkipLayer = 4;
+constexpr int kPeSteps = 32;                        // PE padded 63 -> 64 inputs = 32 k-steps
+constexpr int kActSteps = kHidden / 2;              // 256 inputs = 128 k-steps
+constexpr int kRayFeat = 2 * kDirHidden;            // per-ray [dir part | appearance part]
+
+// Matrices held as fragments: 0 = layer 0 (PE input), 1..7 = the 256 activation inputs of
+// trunk layers 1..7, 8 = the h-part of dir_linear, 9 = the PE part of the skip layer
+// (layer 4 input is cat[h, enc_x], models.py:130-131).
+constexpr int kNumFragMats = 10;
+constexpr int kSkipPeMat = 9;
+NERF_HD constexpr bool frag_is_pe(int m) { return m == 0 || m == kSkipPeMat; }
+NERF_HD constexpr int frag_ntiles(int m) { return m == 8 ? 4 : 8; }
+NERF_HD constexpr int frag_act_steps(int m) { return frag_is_pe(m) ? 0 : kActSteps; }
+NERF_HD constexpr int frag_pe_steps(int m) { return frag_is_pe(m) ? kPeSteps : 0; }
+NERF_HD constexpr int frag_ksteps(int m) { return frag_act_steps(m) + frag_pe_steps(m); }
+NERF_HD constexpr size_t frag_floats(int m) { return (size_t)frag_ntiles(m) * frag_ksteps(m) * 64; }
+NERF_HD constexpr size_t frag_offset(int m) {
+  size_t off = 0;
+  for (int i = 0; i < m; ++i) off += frag_floats(i);
+  return off;
+}
+constexpr size_t kFragFloats = frag_offset(kNumFragMats);   // 524288 floats = 2 MiB
+
+// Raw vectors after the fragments (each rounded up to 4 floats for 16-B loads).
+constexpr size_t kOffBias = kFragFloats;                        // 8 x 256 trunk biases
+constexpr size_t kOffSigmaW = kOffBias + 8 * kHidden;           // density_head.weight (256)
+constexpr size_t kOffSigmaB = kOffSigmaW + kHidden;             // density_head.bias (1, padded 4)
+constexpr size_t kOffDirB = kOffSigmaB + 4;                     // dir_linear.bias (128)
+constexpr size_t kOffDirWd = kOffDirB + kDirHidden;             // dir_linear.weight[:,256:283] (128 x 27)
+constexpr size_t kOffAppW = kOffDirWd + kDirHidden * kDirEnc;   // appearance_projection.weight (128 x 32)
+constexpr size_t kOffAppB = kOffAppW + kDirHidden * kAppDim;    // appearance_projection.bias (128)
+constexpr size_t kOffRgbW = kOffAppB + kDirHidden;              // rgb_linear.weight (3 x 128)
+constexpr size_t kOffRgbB = kOffRgbW + 3 * kDirHidden;          // rgb_linear.bias (3, padded 4)
+constexpr size_t kPackedFloats = kOffRgbB + 4;
+
+// Index of a state_dict tensor in the 24-pointer parameter list of nerf_pack_weights.
+enum Param {
+  P_PTS_W0 = 0,  // pts_linears.i.weight = 2i, .bias = 2i+1
+  P_SIGMA_W = 16, P_SIGMA_B, P_DIR_W, P_DIR_B, P_APP_W, P_APP_B, P_RGB_W, P_RGB_B, P_COUNT
+};
+
+// Positional-encoding input of PE k-step p for lane half h (reference feature order,
+// models.py:36-44: [x, sin(x), cos(x), sin(2x), cos(2x), ...] in blocks of 3).
+// Steps 0..29: frequency i = p/3, component c = p%3; half 0 carries sin, half 1 cos.
+// Step 30: x0 | x1.  Step 31: x2 | padding (-1).
+NERF_HD inline int pe_feature(int p, int h) {
+  if (p < 3 * kPosLevels) {
+    const int i = p / 3, c = p % 3;
+    return 3 + 6 * i + (h ? 3 : 0) + c;
+  }
+  if (p == 30) return h ? 1 : 0;
+  return h ? -1 : 2;
+}
+
+// Input column of the activation k-step ks (0..127) for lane half h: register g of
+// accumulator tile t of the previous layer holds neuron 32t + (g&3) + 8(g>>2) + 4h.
+NERF_HD inline int act_feature(int ks, int h) {
+  const int t = ks >> 4, g = ks & 15;
+  return 32 * t + (g & 3) + 8 * (g >> 2) + 4 * h;
+}
+
+// Source of packed fragment element (matrix m, n-tile nt, k-step ks, lane l):
+// returns the column of W (row nt*32 + (l&31)) or -1 for zero padding.
+NERF_HD inline int frag_source_col(int m, int ks, int lane) {
+  const int h = lane >> 5;
+  const int act = frag_act_steps(m);
+  if (ks < act) return act_feature(ks, h);
+  const int f = pe_feature(ks - act, h);
+  if (f < 0) return -1;
+  return (m == kSkipPeMat ? kHidden : 0) + f;   // skip layer input is cat[h, enc_x] (models.py:131)
+}
+
+}  // namespace nerf
+
+namespace nerf {
+// Float offset, inside matrix m's fragment array, of element j of lane `lane` in the
+// fragment block (n-tile nt, k-step quad kq): ks = 4*kq + j.
+NERF_HD inline size_t frag_elem(int m, int nt, int kq, int lane, int j) {
+  return frag_offset(m) + ((size_t)(nt * (frag_ksteps(m) / 4) + kq) * 64 + lane) * 4 + j;
+}
+}  // namespace nerf

@@ -1,0 +1,162 @@
+"""CPU-side checks of libnerfmi.so: it loads, exports every symbol include/nerfmi.h declares,
+rejects bad arguments without touching a GPU, and its weight packer produces the layout the
+MLP kernel assumes.  The last part replays the kernel's register dataflow (layout.h) in numpy
+on the host-packed buffer and compares with the oracle's NeRF.forward."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import torch
+
+from conftest import REPO
+from oracle import nerf_oracle as O
+from nerfmi import _lib
+
+HEADER = os.path.join(REPO, "include", "nerfmi.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(nerf_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/nerfmi.h"
+    assert lib.nerf_abi_version() == 1
+
+
+def test_bad_arguments_are_reported_not_launched():
+    lib = _lib.load()
+    rc = lib.nerf_composite(None, None, None, 10, 64, None, None, None, None)
+    assert rc == 1 and b"null pointer" in lib.nerf_last_error()
+    rc = lib.nerf_composite(None, None, None, 10, 5000, None, None, None, None)
+    assert rc == 3
+    rc = lib.nerf_sample_importance(None, None, None, None, 4, 300, 128, None, None, 0, None, None, None)
+    assert rc == 3
+    rc = lib.nerf_mlp_forward(None, None, None, None, 4, 2, None, None, None, None)
+    assert rc == 1 and b"N must be 1" in lib.nerf_last_error()
+    assert lib.nerf_render_workspace_bytes(0, 64, 128) == 0 or lib.nerf_render_workspace_bytes(0, 64, 128) >= 0
+    assert lib.nerf_render_workspace_bytes(-1, 64, 0) == 0
+    # empty inputs are a no-op, not an error
+    assert lib.nerf_composite(None, None, None, 0, 64, None, None, None, None) == 0
+
+
+def host_pack(state):
+    lib = _lib.load()
+    ts = [state[k].contiguous().float() for k in O.STATE_KEYS]
+    arr = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    out = np.empty(lib.nerf_packed_weights_floats(), dtype=np.float32)
+    assert lib.nerf_pack_weights_host(arr, out.ctypes.data) == 0
+    return out
+
+
+# ---- restatement of csrc/layout.h for the emulator
+PE_STEPS, ACT_STEPS = 32, 128
+
+
+def frag_ntiles(m):
+    return 4 if m == 8 else 8
+
+
+def frag_ksteps(m):
+    return PE_STEPS if m in (0, 9) else ACT_STEPS
+
+
+def frag_offset(m):
+    return sum(frag_ntiles(i) * frag_ksteps(i) * 64 for i in range(m))
+
+
+def pe_feature(p, h):
+    if p < 30:
+        i, c = divmod(p, 3)
+        return 3 + 6 * i + (3 if h else 0) + c
+    if p == 30:
+        return 1 if h else 0
+    return -1 if h else 2
+
+
+def act_feature(ks, h):
+    t, g = divmod(ks, 16)
+    return 32 * t + (g & 3) + 8 * (g >> 2) + 4 * h
+
+
+def frag_matrix(packed, m):
+    """W as the kernel sees it: [n][slot], slot = 2*ks + h (k-step ks, lane half h)."""
+    nt, ks = frag_ntiles(m), frag_ksteps(m)
+    blk = packed[frag_offset(m): frag_offset(m) + nt * ks * 64].reshape(nt, ks // 4, 2, 32, 4)
+    # [nt][kq][h][n%32][j] -> [n][kq][j][h]
+    return blk.transpose(0, 3, 1, 4, 2).reshape(nt * 32, ks * 2).astype(np.float64)
+
+
+def test_packed_fragments_are_permuted_weights(ref_state):
+    packed = host_pack(ref_state)
+    W = {m: ref_state[f"pts_linears.{m}.weight"].numpy() for m in range(8)}
+    for m in range(1, 8):
+        Wp = frag_matrix(packed, m)
+        cols = [act_feature(s // 2, s % 2) for s in range(2 * ACT_STEPS)]
+        assert np.array_equal(Wp, W[m][:, cols]), m
+    Wp = frag_matrix(packed, 0)
+    for s in range(64):
+        f = pe_feature(s // 2, s % 2)
+        assert np.array_equal(Wp[:, s], W[0][:, f] if f >= 0 else np.zeros(256)), s
+    Wp = frag_matrix(packed, 9)
+    for s in range(64):
+        f = pe_feature(s // 2, s % 2)
+        assert np.array_equal(Wp[:, s], W[4][:, 256 + f] if f >= 0 else np.zeros(256)), s
+    Wd = ref_state["dir_linear.weight"].numpy()
+    cols = [act_feature(s // 2, s % 2) for s in range(2 * ACT_STEPS)]
+    assert np.array_equal(frag_matrix(packed, 8), Wd[:, cols])
+
+
+def emulate_forward(packed, x, d, app):
+    """The kernel's dataflow (csrc/mlp.hip) in float64 on the packed buffer."""
+    off_bias = frag_offset(10)
+    off_sw = off_bias + 8 * 256
+    off_sb = off_sw + 256
+    off_db = off_sb + 4
+    off_dwd = off_db + 128
+    off_aw = off_dwd + 128 * 27
+    off_ab = off_aw + 128 * 32
+    off_rw = off_ab + 128
+    off_rb = off_rw + 3 * 128
+    p = packed.astype(np.float64)
+    enc = O.positional_encoding(torch.from_numpy(x), 10).numpy().astype(np.float64)
+    pe_slots = np.stack([enc[:, pe_feature(s // 2, s % 2)] if pe_feature(s // 2, s % 2) >= 0
+                         else np.zeros(len(x)) for s in range(64)], 1)
+
+    def act_slots(h):
+        return h[:, [act_feature(s // 2, s % 2) for s in range(256)]]
+
+    bias = p[off_bias: off_bias + 8 * 256].reshape(8, 256)
+    h = np.maximum(pe_slots @ frag_matrix(packed, 0).T + bias[0], 0)
+    for m in range(1, 8):
+        pre = act_slots(h) @ frag_matrix(packed, m).T + bias[m]
+        if m == 4:
+            pre += pe_slots @ frag_matrix(packed, 9).T
+        h = np.maximum(pre, 0)
+    sigma = np.maximum(h @ p[off_sw: off_sw + 256] + p[off_sb], 0)
+    encd = O.positional_encoding(torch.from_numpy(d), 4).numpy().astype(np.float64)
+    dvec = p[off_db: off_db + 128] + encd @ p[off_dwd: off_dwd + 128 * 27].reshape(128, 27).T
+    appf = np.zeros(128) if app is None else p[off_ab: off_ab + 128] + app.astype(np.float64) @ \
+        p[off_aw: off_aw + 128 * 32].reshape(128, 32).T
+    hd = np.maximum(act_slots(h) @ frag_matrix(packed, 8).T + dvec, 0) + appf
+    rgb = 1 / (1 + np.exp(-(hd @ p[off_rw: off_rw + 384].reshape(3, 128).T + p[off_rb: off_rb + 3])))
+    return rgb, sigma[:, None]
+
+
+def test_emulated_kernel_matches_oracle(ref_state, app_vec):
+    packed = host_pack(ref_state)
+    torch.manual_seed(5)
+    x = torch.randn(256, 3) * 2
+    d = torch.nn.functional.normalize(torch.randn(256, 3), dim=-1)
+    for app in (None, app_vec):
+        rgb, sigma = emulate_forward(packed, x.numpy(), d.numpy(), None if app is None else app.numpy())
+        rgb_o, sigma_o = O.nerf_forward(ref_state, x, d, app)
+        np.testing.assert_allclose(rgb, rgb_o.numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(sigma, sigma_o.numpy(), rtol=1e-4, atol=1e-6)

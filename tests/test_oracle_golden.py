@@ -1,0 +1,119 @@
+"""The oracle against the reference's own outputs (tests/golden, made by make_golden.py).
+
+Every comparison here is bit-exact: the oracle restates the reference on the same CPU
+arithmetic, so any difference is a restatement bug."""
+import numpy as np
+import torch
+
+from conftest import seeded_uniform
+from oracle import nerf_oracle as O
+from nerfmi import cameras
+
+
+def test_weights_regenerate(ref_state, golden_meta):
+    shapes = [list(ref_state[k].shape) for k in O.STATE_KEYS]
+    assert shapes == golden_meta["F0"]["shapes"]
+    assert list(O.STATE_KEYS) == golden_meta["F0"]["keys"]
+
+
+def test_nerfmi_model_draws_reference_weights(ref_state):
+    import nerfmi
+    torch.manual_seed(0)
+    m = nerfmi.NeRF(nerfmi.Config())
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(O.STATE_KEYS)
+    for k in O.STATE_KEYS:
+        assert torch.equal(sd[k], ref_state[k]), k
+
+
+def test_poses_and_focal(golden, golden_meta):
+    f1 = golden("f1_get_rays.npz")
+    assert cameras.synthetic_focal(800) == golden_meta["F1"]["focal"]
+    for scene in ("chair", "hotdog"):
+        assert np.array_equal(cameras.frame_c2w(scene).numpy(), f1[f"{scene}_c2w"])
+
+
+def test_get_rays(golden, golden_meta):
+    f1 = golden("f1_get_rays.npz")
+    for scene in ("chair", "hotdog"):
+        o, d = O.get_rays(800, 800, golden_meta["F1"]["focal"], torch.from_numpy(f1[f"{scene}_c2w"]))
+        assert o.stride() == (0, 0, 1) or o.stride()[:2] == (0, 0)
+        assert np.array_equal(o[368:432, 368:432].reshape(-1, 3).numpy(), f1[f"{scene}_o"])
+        assert np.array_equal(d[368:432, 368:432].reshape(-1, 3).numpy(), f1[f"{scene}_d"])
+    o, d = O.get_rays(5, 7, 123.4, torch.from_numpy(f1["small_c2w"]))
+    assert list(o.stride()) == golden_meta["F1"]["small"]["origin_stride"]
+    assert np.array_equal(o.contiguous().numpy(), f1["small_o"])
+    assert np.array_equal(d.numpy(), f1["small_d"])
+
+
+def test_forward(golden, ref_state, app_vec):
+    f2 = golden("f2_forward.npz")
+    x, d = torch.from_numpy(f2["x"]), torch.from_numpy(f2["d"])
+    cases = (("none", None, 1024), ("app2d", app_vec[None], 1024), ("app1d", app_vec, 1024),
+             ("per_sample", torch.from_numpy(f2["app_per_sample"]), 512))
+    for name, a, n in cases:
+        rgb, sigma = O.nerf_forward(ref_state, x[:n], d[:n], a)
+        assert np.array_equal(rgb.numpy(), f2[f"rgb_{name}"]), name
+        assert np.array_equal(sigma.numpy(), f2[f"sigma_{name}"]), name
+
+
+def _crop(golden, scene):
+    f1 = golden("f1_get_rays.npz")
+    return torch.from_numpy(f1[f"{scene}_o"]), torch.from_numpy(f1[f"{scene}_d"])
+
+
+def test_volume_render_coarse(golden, ref_state, app_vec):
+    f3 = golden("f3_coarse.npz")
+    o, d = _crop(golden, "chair")
+    rgb, depth, ex = O.volume_render(ref_state, o, d, 2.0, 6.0, 64, app_vec)
+    assert np.array_equal(rgb.numpy(), f3["chair_rgb"])
+    assert np.array_equal(depth.numpy(), f3["chair_depth"])
+    assert np.array_equal(ex["weights"][:256, :, 0].numpy(), f3["chair_weights256"])
+    assert np.array_equal(ex["z_vals"][0].numpy(), f3["z_row"])
+    rgb, depth, _ = O.volume_render(ref_state, o[:1024], d[:1024], 2.0, 6.0, 64, None)
+    assert np.array_equal(rgb.numpy(), f3["chair_noapp_rgb"])
+    rgb, depth, _ = O.volume_render(ref_state, o[:1024], d[:1024], 2.0, 6.0, 32, app_vec)
+    assert np.array_equal(rgb.numpy(), f3["chair_n32_rgb"])
+    oh, dh = _crop(golden, "hotdog")
+    rgb, depth, _ = O.volume_render(ref_state, oh[:1024], dh[:1024], 2.0, 6.0, 64, app_vec)
+    assert np.array_equal(rgb.numpy(), f3["hotdog_rgb"])
+    assert np.array_equal(depth.numpy(), f3["hotdog_depth"])
+
+
+def test_volume_render_perturb(golden, golden_meta, ref_state, app_vec):
+    f4 = golden("f4_perturb.npz")
+    m = golden_meta["F4"]
+    t_rand = seeded_uniform(m["seed"], m["t_rand_shape"], m["t_rand_sha256"])
+    o, d = _crop(golden, "chair")
+    rgb, depth, ex = O.volume_render(ref_state, o[:1024], d[:1024], 2.0, 6.0, 64, app_vec, t_rand=t_rand)
+    assert np.array_equal(rgb.numpy(), f4["rgb"])
+    assert np.array_equal(depth.numpy(), f4["depth"])
+    assert np.array_equal(ex["z_vals"][:128].numpy(), f4["z128"])
+
+
+def test_sample_importance_h1(golden, golden_meta):
+    f5 = golden("f5_importance.npz")
+    m = golden_meta["F5"]
+    u = seeded_uniform(m["seed"], m["u_rand_shape"], m["u_rand_sha256"])
+    args = [torch.from_numpy(f5[k]) for k in ("o", "d", "z", "w")]
+    z_all, pts = O.sample_importance_h1(*args, 128, u)
+    assert np.array_equal(z_all.numpy(), f5["z_all"])
+    assert torch.all(z_all[:, 1:] >= z_all[:, :-1])
+    # the input on which the reference raises: H1 gives the trick-3 result
+    assert m["ref_raises_on_last_bin"]
+    u = seeded_uniform(12, (2, 128), m["u_bad_sha256"])
+    z_all, _ = O.sample_importance_h1(args[0][:2], args[1][:2], args[2][:2], torch.from_numpy(f5["w_bad"]), 128, u)
+    assert np.array_equal(z_all.numpy(), f5["z_bad_all"])
+
+
+def test_hierarchical_h1(golden, golden_meta, ref_state, app_vec):
+    f6 = golden("f6_hierarchical.npz")
+    m = golden_meta["F6"]
+    u = seeded_uniform(m["seed"], m["u_rand_shape"], m["u_rand_sha256"])
+    o, d = _crop(golden, "chair")
+    rgb, depth, ex = O.render_rays_h1(ref_state, o[:1024], d[:1024], 2.0, 6.0, 64, 128, app_vec, None, u)
+    assert np.array_equal(rgb.numpy(), f6["rgb"])
+    assert np.array_equal(depth.numpy(), f6["depth"])
+    assert np.array_equal(ex["rgb_map_coarse"].numpy(), f6["rgb_coarse"])
+    assert np.array_equal(ex["z_vals"][:64].numpy(), f6["z_all64"])
+    assert np.array_equal(ex["weights"][:64, :, 0].numpy(), f6["weights64"])
