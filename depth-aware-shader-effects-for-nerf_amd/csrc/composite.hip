@@ -9,6 +9,10 @@
 // 64-sample chunk, the running product carried across chunks).  Sums accumulate the
 // reference's float products in double and round once.
 //
+// N == 1 reproduces the reference's degenerate case: z[1:]-z[:-1] is empty and so is the
+// padded dists tensor (render.py:56-58 pads with ones_like of an empty slice), every
+// per-sample tensor is empty and both maps are 0.
+//
 // Bound: HBM.  Reads 20 B/sample (rgb 12, sigma 4, z 4), writes 16 B/ray (+4 B/sample of
 // weights when requested).  Consecutive lanes touch consecutive samples of one ray.
 #include "common.h"
@@ -31,7 +35,9 @@ composite_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma,
   const int64_t base = r * N;
   double carry = 1.0;
   double acc_r = 0.0, acc_g = 0.0, acc_b = 0.0, acc_wz = 0.0, acc_w = 0.0;
-  for (int c0 = 0; c0 < N; c0 += 64) {
+  if (N == 1 && weights && lane == 0) weights[base] = 0.0f;
+  const int n_eff = N > 1 ? N : 0;
+  for (int c0 = 0; c0 < n_eff; c0 += 64) {
     const int s = c0 + lane;
     const bool valid = s < N;
     float alpha = 0.0f, z = 0.0f;

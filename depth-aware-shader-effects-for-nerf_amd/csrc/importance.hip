@@ -8,14 +8,15 @@
 //     with denom = cdf[above]-cdf[below], 1 where < 1e-5, and below'/above' the z index
 //     clamped to N-1 (H1: the reference gathers z[N] there and raises).
 //   z_all = sort(cat[z, z_f]);  pts = o + d*z_all                           (:142-147)
-// cumsum runs as a double-precision add scan (torch's CPU cumsum accumulates in double).
+// cumsum runs as a double-precision add scan (torch's CPU cumsum accumulates in double; the
+// double partial sums of these floats are exact, so the association order does not matter).
 // The merge computes every element's output slot by binary search in the other sorted list
 // (merge path); if either list is not ascending (possible by one rounding step in
 // degenerate bins) every slot is instead the element's full rank, so the output is always
 // exactly sort(cat[z, z_f]).
 //
 // Bound: HBM/latency.  Reads 8 B per coarse sample (+4 B per fine uniform), writes 4 B per
-// merged sample (+12 B with pts).  LDS per wave: (N+1) + N + Nf floats.
+// merged sample (+12 B with pts).  LDS per wave: (N+1) + 2N + Nf floats.
 #include "common.h"
 
 namespace nerf {
@@ -54,17 +55,40 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * 4 + wid;
-  const int per_wave = (N + 1) + N + Nf;
+  const int per_wave = (N + 1) + N + Nf + N;
   float* cdf = lds + wid * per_wave;
   float* zc = cdf + (N + 1);
   float* zf = zc + N;
+  float* wp = zf + Nf;
   const bool live = r < B;                     // dead waves still reach every barrier
   const int64_t rr = live ? r : 0;
 
-  // pdf normaliser (:106-108)
-  double part = 0.0;
-  for (int s = lane; s < N; s += 64) part += (double)(wv[rr * N + s] + 1e-5f);
-  const float total = (float)wave_sum_d(part);
+  // pdf normaliser (:106-108), summed in the order torch's CPU sum reduces a contiguous float
+  // row (aten SumKernel: 8-float vectors, 4 interleaved vector accumulators, then the scalar
+  // tail and the 8 lanes left to right), so pdf and cdf come out bit-identical.
+  for (int s = lane; s < N; s += 64) wp[s] = wv[rr * N + s] + 1e-5f;
+  __syncthreads();
+  const int nvec = N >> 3, ilp = nvec >> 2;
+  float part = 0.0f;
+  if (lane < 32) {
+    const int k = lane >> 3, l = lane & 7;
+    for (int i = 0; i < ilp; ++i) part += wp[(i * 4 + k) * 8 + l];
+    if (k == 0)
+      for (int i = ilp * 4; i < nvec; ++i) part += wp[i * 8 + l];
+  }
+  const float vsum = ((part + __shfl(part, lane + 8)) + __shfl(part, lane + 16)) + __shfl(part, lane + 24);
+  float total = 0.0f;
+  if (nvec > 0) {
+    for (int s = nvec * 8; s < N; ++s) total += wp[s];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) total += __shfl(vsum, l);
+  } else {  // rows shorter than one vector: 4 interleaved scalar accumulators
+    float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < (N >> 2); ++i)
+      for (int k = 0; k < 4; ++k) p[k] += wp[4 * i + k];
+    for (int s = (N >> 2) * 4; s < N; ++s) p[0] += wp[s];
+    total = ((p[0] + p[1]) + p[2]) + p[3];
+  }
 
   // cdf = [0, cumsum(pdf)] (:111-112), z to LDS
   double carry = 0.0;
@@ -72,7 +96,7 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
     const int s = c0 + lane;
     double v = 0.0;
     if (s < N) {
-      v = (double)((wv[rr * N + s] + 1e-5f) / total);
+      v = (double)(wp[s] / total);
       zc[s] = zv[rr * N + s];
     }
 #pragma unroll
@@ -145,7 +169,7 @@ int launch_importance(const float* o, const float* d, const float* z, const floa
                       const float* u_lin, const float* u_rand, uint64_t seed, float* z_all, float* pts_all,
                       hipStream_t s) {
   if (B == 0) return NERF_OK;
-  const size_t lds = (size_t)4 * ((N + 1) + N + Nf) * sizeof(float);
+  const size_t lds = (size_t)4 * ((N + 1) + 2 * N + Nf) * sizeof(float);
   hipLaunchKernelGGL(importance_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), lds, s, o, d, z, w, B, N, Nf,
                      u_lin, u_rand, seed, z_all, pts_all);
   return check_launch("importance_kernel");

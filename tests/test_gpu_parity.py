@@ -5,7 +5,9 @@ Tolerances (north star: 1e-4 relative fp32 on rgb/depth, bit-exact ray indices):
   * rgb / depth / weights / sigma: |gpu - ref| <= 1e-4*|ref| + 1e-6 (the 1e-6 floor because
     random-init rgb is ~0.03 and accumulations of ~64-256 terms differ in order);
   * PE features: |gpu - ref| <= 2e-6 (sin/cos are 1-2 ulp functions on both sides);
-  * fine z (inverse CDF): 1e-6 relative (prefix sums in a different association order).
+  * fine z (inverse CDF) from the same coarse weights: bit-exact (the pdf normaliser is summed
+    in torch's CPU order and the double prefix sums are exact); behind a GPU-computed coarse pass
+    the weights already differ by ~1e-6 relative, so z there is held to 1e-5 relative.
 """
 import numpy as np
 import pytest
@@ -142,7 +144,10 @@ def test_composite_kernel(ref_state):
         r_ref, d_ref, w_ref = O.composite(rgb, sigma[..., None], z)
         close(rm, r_ref, what=f"rgb B={B} N={N}")
         close(dm, d_ref[:, 0], what=f"depth B={B} N={N}")
-        close(wm, w_ref[..., 0], what=f"weights B={B} N={N}")
+        if N > 1:
+            close(wm, w_ref[..., 0], what=f"weights B={B} N={N}")
+        else:   # the reference's weights are empty at N=1; the kernel writes zeros
+            assert w_ref.shape[1] == 0 and not wm.any()
 
 
 # --------------------------------------------------------------------------- volume_render
@@ -189,8 +194,7 @@ def test_sample_importance(nerfmi_mod, golden, golden_meta):
     u = seeded_uniform(m["seed"], m["u_rand_shape"], m["u_rand_sha256"])
     o, d, z, w = (torch.from_numpy(f5[k]).cuda() for k in ("o", "d", "z", "w"))
     z_all, pts = nerfmi_mod.sample_importance(o, d, z, w, 128, u_rand=u)
-    close(z_all, f5["z_all"], rtol=1e-6, atol=0, what="z_all")
-    assert float((z_all.cpu().numpy() == f5["z_all"]).mean()) > 0.99
+    assert np.array_equal(z_all.cpu().numpy(), f5["z_all"])
     assert bool((z_all[:, 1:] >= z_all[:, :-1]).all())
     za = z_all.cpu()
     assert torch.equal(pts.cpu(), o.cpu()[:, None, :] + d.cpu()[:, None, :] * za[..., None])
@@ -198,7 +202,22 @@ def test_sample_importance(nerfmi_mod, golden, golden_meta):
     u = seeded_uniform(12, (2, 128), m["u_bad_sha256"])
     w_bad = torch.from_numpy(f5["w_bad"]).cuda()[..., None]
     z_all, _ = nerfmi_mod.sample_importance(o[:2], d[:2], z[:2], w_bad, 128, u_rand=u)
-    close(z_all, f5["z_bad_all"], rtol=1e-6, atol=0, what="z_bad_all")
+    assert np.array_equal(z_all.cpu().numpy(), f5["z_bad_all"])
+
+
+def test_sample_importance_shapes_vs_oracle(nerfmi_mod):
+    torch.manual_seed(12)
+    for B, N, Nf in ((33, 64, 128), (5, 7, 9), (7, 100, 64), (3, 256, 1024), (4, 1, 16), (2, 64, 1)):
+        o = torch.randn(B, 3)
+        d = torch.nn.functional.normalize(torch.randn(B, 3), dim=-1)
+        z = torch.sort(torch.rand(B, N) * 4 + 2, dim=-1).values
+        w = torch.rand(B, N) * (torch.rand(B, N) > 0.5)
+        w[0] = 0                      # all-zero weights: a uniform pdf
+        u = torch.rand(B, Nf)
+        z_all, pts = nerfmi_mod.sample_importance(o.cuda(), d.cuda(), z.cuda(), w.cuda(), Nf, u_rand=u)
+        z_ref, pts_ref = O.sample_importance_h1(o, d, z, w, Nf, u)
+        assert torch.equal(z_all.cpu(), z_ref), (B, N, Nf)
+        assert torch.equal(pts.cpu(), pts_ref), (B, N, Nf)
 
 
 def test_hierarchical_h1(nerfmi_mod, model, golden, golden_meta, app_vec):
@@ -212,7 +231,7 @@ def test_hierarchical_h1(nerfmi_mod, model, golden, golden_meta, app_vec):
     close(rgb, f6["rgb"], what="fine rgb")
     close(depth, f6["depth"], what="fine depth")
     close(ex["rgb_map_coarse"], f6["rgb_coarse"], what="coarse rgb")
-    close(ex["z_vals"][:64], f6["z_all64"], rtol=1e-6, atol=0, what="z_all")
+    close(ex["z_vals"][:64], f6["z_all64"], rtol=1e-5, atol=0, what="z_all")
     close(ex["weights"][:64, :, 0], f6["weights64"], what="fine weights")
     # the staged path (per-stage entry points) runs the same kernels: identical bits
     timing = []
@@ -244,7 +263,16 @@ def test_edge_sizes(nerfmi_mod, model, ref_state, app_vec):
 
 def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_meta):
     """800x800 hierarchical 64+128 (the bench workload): size-independent properties on every ray,
-    and oracle parity on 1024 rays sampled across the frame."""
+    and oracle parity on 4096 rays sampled across the frame.
+
+    The fine pass is ill-conditioned in the coarse weights: the inverse CDF moves a fine sample by
+    ~4x the relative change of the weights, and the 2^9 positional-encoding frequency turns that
+    into phase.  GPU and CPU coarse weights differ at ~1e-5 relative (summation order inside the
+    MLP), so a handful of rays per thousand differ by up to a few 1e-4 relative end to end
+    (test_fine_pass_conditioning shows the oracle moves the same way under a 1-ulp perturbation
+    of its own weights).  Parity is therefore asserted (a) at 1e-4 for every ray with the fine
+    samples held equal (the oracle's fine pass on the GPU's z), and (b) end to end as PSNR
+    > 80 dB, >= 99.5% of values inside 1e-4 and none beyond 1e-3 relative."""
     from nerfmi import cameras
     c2w = cameras.frame_c2w("chair").cuda()
     o, d = nerfmi_mod.get_rays(800, 800, golden_meta["F1"]["focal"], c2w)
@@ -260,8 +288,22 @@ def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_met
     wsum = ex["weights"][..., 0].sum(-1)
     assert float(wsum.max()) <= 1 + 1e-5
     assert float(depth.min()) >= 2.0 - 1e-4 and float(depth.max()) <= 6.0 + 1e-4
-    idx = torch.randperm(o.shape[0])[:1024]
-    r_ref, d_ref, _ = O.render_rays_h1(ref_state, o[idx].cpu(), d[idx].cpu(), 2.0, 6.0, 64, 128, app_vec, None,
-                                       u[idx])
-    close(rgb[idx], r_ref, what="frame rgb")
-    close(depth[idx], d_ref, what="frame depth")
+    idx = torch.randperm(o.shape[0])[:4096]
+    oc, dc = o[idx].cpu(), d[idx].cpu()
+    # (a) fine samples held equal
+    dn = O.normalize(dc)
+    zg = z[idx].cpu()
+    pts = oc[:, None, :] + dn[:, None, :] * zg[..., None]
+    r_fix, d_fix, _ = O._pass(ref_state, pts, dn, zg, app_vec)
+    close(rgb[idx], r_fix, what="fine rgb, same z")
+    close(depth[idx], d_fix, what="fine depth, same z")
+    # (b) end to end
+    r_ref, d_ref, ex_ref = O.render_rays_h1(ref_state, oc, dc, 2.0, 6.0, 64, 128, app_vec, None, u[idx])
+    close(ex["rgb_map_coarse"][idx], ex_ref["rgb_map_coarse"], what="coarse rgb")
+    g = rgb[idx].cpu()
+    err = (g - r_ref).abs()
+    inside = (err <= 1e-6 + 1e-4 * r_ref.abs()).float().mean()
+    psnr = -10 * torch.log10(((g - r_ref) ** 2).mean())
+    assert float(psnr) > 80, float(psnr)
+    assert float(inside) >= 0.995, float(inside)
+    assert float((err / r_ref.abs()).max()) < 1e-3
