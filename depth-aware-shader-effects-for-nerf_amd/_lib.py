@@ -31,6 +31,11 @@ _SIGNATURES = {
                                               ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p]),
+    "nerf_sample_importance_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nerf_packed_weights_floats": (ctypes.c_size_t, []),
     "nerf_pack_weights": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p]),
     "nerf_pack_weights_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
@@ -38,7 +43,7 @@ _SIGNATURES = {
                                          ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "nerf_mlp_forward": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p, ctypes.c_void_p]),
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "nerf_composite": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]),
@@ -53,6 +58,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
+ABI_VERSION = 2
 
 _lib = None
 
@@ -69,6 +75,9 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.nerf_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"nerfmi: {LIB_PATH} has ABI {lib.nerf_abi_version()}, this package needs "
+                               f"{ABI_VERSION}; rebuild it")
         _lib = lib
     return _lib
 

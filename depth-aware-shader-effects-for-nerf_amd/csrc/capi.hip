@@ -85,7 +85,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 1; }
+int nerf_abi_version(void) { return 2; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -129,7 +129,21 @@ int nerf_sample_importance(const float* rays_o, const float* rays_d, const float
   REQUIRE(B == 0 || (z_vals && weights && u_lin && z_all), "nerf_sample_importance: null pointer");
   REQUIRE(!pts_all || (rays_o && rays_d), "nerf_sample_importance: pts requested without rays");
   return launch_importance(rays_o, rays_d, z_vals, weights, B, N, Nf, u_lin, u_rand, seed, z_all, pts_all,
-                           (hipStream_t)stream);
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int nerf_sample_importance_merge(const float* z_vals, const float* weights, const float* rgb_c,
+                                 const float* sigma_c, int64_t B, int N, int Nf, const float* u_lin,
+                                 const float* u_rand, uint64_t seed, float* z_all, float* rgb_all,
+                                 float* sigma_all, float* z_fine, int32_t* fine_slot, nerf_stream_t stream) {
+  REQUIRE(B >= 0, "nerf_sample_importance_merge: B=%lld", (long long)B);
+  if (N < 1 || N > 256 || Nf < 1 || Nf > 1024)
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_sample_importance_merge: N=%d (1..256) Nf=%d (1..1024)", N, Nf);
+  REQUIRE(B == 0 || (z_vals && weights && rgb_c && sigma_c && u_lin && z_all && rgb_all && sigma_all && z_fine &&
+                     fine_slot),
+          "nerf_sample_importance_merge: null pointer");
+  return launch_importance(nullptr, nullptr, z_vals, weights, B, N, Nf, u_lin, u_rand, seed, z_all, nullptr, rgb_c,
+                           sigma_c, rgb_all, sigma_all, z_fine, fine_slot, (hipStream_t)stream);
 }
 
 size_t nerf_packed_weights_floats(void) { return kPackedFloats; }
@@ -157,12 +171,14 @@ int nerf_ray_features(const float* packed, const float* dirs, int64_t R, const f
 }
 
 int nerf_mlp_forward(const float* packed, const float* origins, const float* dirs, const float* z_vals, int64_t R,
-                     int N, const float* ray_feat, float* rgb, float* sigma, nerf_stream_t stream) {
+                     int N, const float* ray_feat, float* rgb, float* sigma, const int32_t* out_slot, int out_T,
+                     nerf_stream_t stream) {
   REQUIRE(R >= 0 && N >= 1, "nerf_mlp_forward: R=%lld N=%d", (long long)R, N);
+  REQUIRE(!out_slot || out_T >= N, "nerf_mlp_forward: out_T=%d < N=%d", out_T, N);
   REQUIRE(z_vals || N == 1, "nerf_mlp_forward: without z_vals the origins are the points and N must be 1");
   REQUIRE(R == 0 || (packed && origins && ray_feat && rgb && sigma && (!z_vals || dirs)),
           "nerf_mlp_forward: null pointer");
-  return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, (hipStream_t)stream);
+  return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, out_slot, out_T, (hipStream_t)stream);
 }
 
 int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, int64_t B, int N, float* rgb_map,
@@ -173,24 +189,26 @@ int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, in
   return launch_composite(rgb, sigma, z_vals, B, N, rgb_map, depth_map, weights, (hipStream_t)stream);
 }
 
-// Workspace carve of nerf_render_rays, in this order (each region 256-B aligned):
-//   dirs (B,3) | z (B,N) | feat (B,256) | rgb (B,T,3) | sigma (B,T) | w (B,N) | z_all (B,T) | maps (B,4)
-// with T = N + Nf.
+// Workspace carve of nerf_render_rays, in this order (each region 256-B aligned), T = N + Nf:
+//   dirs (B,3) | z (B,N) | feat (B,256) | rgb_c (B,N,3) | sigma_c (B,N) | w_c (B,N) | z_all (B,T)
+//   | z_fine (B,Nf) | fine_slot (B,Nf) int32 | rgb_all (B,T,3) | sigma_all (B,T) | maps (B,4)
+enum { W_DIRS, W_Z, W_FEAT, W_RGBC, W_SIGC, W_WC, W_ZALL, W_ZF, W_SLOT, W_RGBA, W_SIGA, W_MAPS, W_COUNT };
+
 static size_t carve(int64_t B, int N, int Nf, size_t* off) {
-  const size_t T = (size_t)N + Nf;
-  const size_t sizes[8] = {(size_t)B * 3, (size_t)B * N, (size_t)B * kRayFeat, (size_t)B * T * 3, (size_t)B * T,
-                           (size_t)B * N, (size_t)B * T, (size_t)B * 4};
+  const size_t T = (size_t)N + Nf, b = (size_t)B;
+  const size_t sizes[W_COUNT] = {b * 3, b * N, b * kRayFeat, b * N * 3, b * N, b * N, b * T,
+                                 b * Nf, b * Nf, b * T * 3, b * T, b * 4};
   size_t at = 0;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < W_COUNT; ++i) {
     off[i] = at;
-    at += align_up(sizes[i] * sizeof(float));
+    at += align_up(sizes[i] * 4);
   }
   return at;
 }
 
 size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf) {
   if (B < 0 || N < 1 || Nf < 0) return 0;
-  size_t off[8];
+  size_t off[W_COUNT];
   return carve(B, N, Nf, off);
 }
 
@@ -208,37 +226,45 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   REQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_render_rays: app_rows=%lld with B=%lld",
           (long long)app_rows, (long long)B);
   REQUIRE(app_rows == 0 || app, "nerf_render_rays: null appearance");
-  size_t off[8];
+  size_t off[W_COUNT];
   const size_t need = carve(B, N, Nf, off);
   if (ws_bytes < need)
     return set_error(NERF_ERR_WORKSPACE, "nerf_render_rays: workspace %zu < %zu bytes", ws_bytes, need);
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  float* dn = (float*)(ws + off[0]);
-  float* z = (Nf == 0 && z_out) ? z_out : (float*)(ws + off[1]);
-  float* feat = (float*)(ws + off[2]);
-  float* rgb = (float*)(ws + off[3]);
-  float* sigma = (float*)(ws + off[4]);
-  float* wc = (Nf == 0) ? weights_out : (float*)(ws + off[5]);
-  float* z_all = z_out ? z_out : (float*)(ws + off[6]);
-  float* maps = (float*)(ws + off[7]);
+  auto region = [&](int i) { return (float*)(ws + off[i]); };
+  float* dn = region(W_DIRS);
+  float* z = (Nf == 0 && z_out) ? z_out : region(W_Z);
+  float* feat = region(W_FEAT);
+  float* rgb_c = region(W_RGBC);
+  float* sigma_c = region(W_SIGC);
+  float* wc = (Nf == 0) ? weights_out : region(W_WC);
+  float* z_all = z_out ? z_out : region(W_ZALL);
+  float* maps = region(W_MAPS);
   int rc;
   if ((rc = launch_normalize(rays_d, B, dn, s))) return rc;                                   // render.py:19
   if ((rc = launch_stratified(rays_o, dn, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed,
                               z, nullptr, s)))
     return rc;                                                                                 // render.py:22
   if ((rc = launch_ray_features(packed, dn, B, app, app_rows, feat, s))) return rc;
-  if ((rc = launch_mlp(packed, rays_o, dn, z, B, N, feat, rgb, sigma, s))) return rc;         // render.py:49
+  if ((rc = launch_mlp(packed, rays_o, dn, z, B, N, feat, rgb_c, sigma_c, nullptr, 0, s))) return rc;  // :49
   if (Nf == 0)
-    return launch_composite(rgb, sigma, z, B, N, rgb_map, depth_map, wc, s);                   // render.py:56-80
+    return launch_composite(rgb_c, sigma_c, z, B, N, rgb_map, depth_map, wc, s);               // render.py:56-80
   float* crgb = coarse_rgb ? coarse_rgb : maps;
   float* cdepth = coarse_depth ? coarse_depth : maps + 3 * B;
-  if ((rc = launch_composite(rgb, sigma, z, B, N, crgb, cdepth, wc, s))) return rc;
-  if ((rc = launch_importance(rays_o, dn, z, wc, B, N, Nf, u_lin, u_rand, seed ^ 0x5DEECE66Dull, z_all, nullptr,
-                              s)))
+  if ((rc = launch_composite(rgb_c, sigma_c, z, B, N, crgb, cdepth, wc, s))) return rc;
+  // H1 fine pass: resample + merge, coarse evaluations reused at their merged slots, the MLP run on
+  // the Nf new samples only, composite over all N+Nf.
+  const int T = N + Nf;
+  float* z_fine = region(W_ZF);
+  int* slot = (int*)region(W_SLOT);
+  float* rgb_all = region(W_RGBA);
+  float* sigma_all = region(W_SIGA);
+  if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed ^ 0x5DEECE66Dull, z_all,
+                              nullptr, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, slot, s)))
     return rc;
-  if ((rc = launch_mlp(packed, rays_o, dn, z_all, B, N + Nf, feat, rgb, sigma, s))) return rc;
-  return launch_composite(rgb, sigma, z_all, B, N + Nf, rgb_map, depth_map, weights_out, s);
+  if ((rc = launch_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_all, sigma_all, slot, T, s))) return rc;
+  return launch_composite(rgb_all, sigma_all, z_all, B, T, rgb_map, depth_map, weights_out, s);
 }
 
 }  // extern "C"

@@ -42,12 +42,14 @@ int launch_stratified(const float* o, const float* d, int64_t B, float near_f, f
                       uint64_t seed, float* z, float* pts, hipStream_t s);
 int launch_importance(const float* o, const float* d, const float* z, const float* w,
                       int64_t B, int N, int Nf, const float* u_lin, const float* u_rand,
-                      uint64_t seed, float* z_all, float* pts_all, hipStream_t s);
+                      uint64_t seed, float* z_all, float* pts_all, const float* rgb_c, const float* sigma_c,
+                      float* rgb_all, float* sigma_all, float* z_fine, int* fine_slot, hipStream_t s);
 int launch_pack(const float* const* params, float* packed, hipStream_t s);
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
                         int64_t app_rows, float* feat, hipStream_t s);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
-               int N, const float* feat, float* rgb, float* sigma, hipStream_t s);
+               int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
+               hipStream_t s);
 int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N,
                      float* rgb_map, float* depth, float* weights, hipStream_t s);
 

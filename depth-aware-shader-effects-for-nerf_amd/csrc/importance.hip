@@ -15,6 +15,12 @@
 // degenerate bins) every slot is instead the element's full rank, so the output is always
 // exactly sort(cat[z, z_f]).
 //
+// Coarse-evaluation reuse (optional outputs): the kernel also scatters the coarse pass's
+// (rgb, sigma) into their merged slots and emits the fine samples with their slots, so the
+// fine MLP pass evaluates only the Nf new samples.  The MLP is deterministic per sample and a
+// coarse sample's point o + d*z is recomputed bit-identically, so this equals re-evaluating all
+// N+Nf merged samples (tests/test_gpu_parity.py::test_coarse_reuse_is_bit_identical).
+//
 // Bound: HBM/latency.  Reads 8 B per coarse sample (+4 B per fine uniform), writes 4 B per
 // merged sample (+12 B with pts).  LDS per wave: (N+1) + 2N + Nf floats.
 #include "common.h"
@@ -50,7 +56,9 @@ __global__ void __launch_bounds__(256)
 importance_kernel(const float* __restrict__ o, const float* __restrict__ d, const float* __restrict__ zv,
                   const float* __restrict__ wv, int64_t B, int N, int Nf, const float* __restrict__ u_lin,
                   const float* __restrict__ u_rand, uint64_t seed, float* __restrict__ z_all,
-                  float* __restrict__ pts_all) {
+                  float* __restrict__ pts_all, const float* __restrict__ rgb_c, const float* __restrict__ sigma_c,
+                  float* __restrict__ rgb_all, float* __restrict__ sigma_all, float* __restrict__ z_fine,
+                  int* __restrict__ fine_slot) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -156,6 +164,18 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
       }
     }
     zo[pos] = v;
+    if (coarse) {
+      if (rgb_all) {                           // coarse evaluation reused at its merged slot
+        const int64_t src = r * N + e, dst = r * T + pos;
+        rgb_all[3 * dst] = rgb_c[3 * src];
+        rgb_all[3 * dst + 1] = rgb_c[3 * src + 1];
+        rgb_all[3 * dst + 2] = rgb_c[3 * src + 2];
+        sigma_all[dst] = sigma_c[src];
+      }
+    } else if (z_fine) {                       // fine sample to evaluate, and where its result goes
+      z_fine[r * Nf + (e - N)] = v;
+      fine_slot[r * Nf + (e - N)] = pos;
+    }
     if (pts_all) {
       float* p = pts_all + 3 * (r * T + pos);
       p[0] = orr.x + drr.x * v;
@@ -167,11 +187,12 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
 
 int launch_importance(const float* o, const float* d, const float* z, const float* w, int64_t B, int N, int Nf,
                       const float* u_lin, const float* u_rand, uint64_t seed, float* z_all, float* pts_all,
-                      hipStream_t s) {
+                      const float* rgb_c, const float* sigma_c, float* rgb_all, float* sigma_all, float* z_fine,
+                      int* fine_slot, hipStream_t s) {
   if (B == 0) return NERF_OK;
   const size_t lds = (size_t)4 * ((N + 1) + 2 * N + Nf) * sizeof(float);
   hipLaunchKernelGGL(importance_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), lds, s, o, d, z, w, B, N, Nf,
-                     u_lin, u_rand, seed, z_all, pts_all);
+                     u_lin, u_rand, seed, z_all, pts_all, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, fine_slot);
   return check_launch("importance_kernel");
 }
 

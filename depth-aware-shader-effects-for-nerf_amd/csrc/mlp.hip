@@ -98,7 +98,7 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
 __global__ void __launch_bounds__(256, 1)
 mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
            const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
-           float* __restrict__ rgb, float* __restrict__ sigma) {
+           float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
   const int lane = threadIdx.x & 63;
   const int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
   if (s0 >= M) return;
@@ -191,19 +191,20 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
     out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
   }
   if (h == 0 && s0 + (lane & 31) < M) {
-    sigma[s] = sig;
+    const int64_t o_s = out_slot ? r * out_T + out_slot[s] : s;
+    sigma[o_s] = sig;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) rgb[3 * s + c] = out[c];
+    for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
   }
 }
 
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
-               const float* feat, float* rgb, float* sigma, hipStream_t s) {
+               const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   const int64_t blocks = (M + 127) / 128;
   hipLaunchKernelGGL(mlp_kernel, dim3((unsigned)blocks), dim3(256), 0, s, packed, o, d, z, M, N, feat, rgb,
-                     sigma);
+                     sigma, out_slot, out_T);
   return check_launch("mlp_kernel");
 }
 

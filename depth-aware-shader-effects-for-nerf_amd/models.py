@@ -151,5 +151,5 @@ def run_mlp(packed, origins, dirs, z_vals, R, N, app, rows, lead, out_device):
     _lib.check(lib.nerf_ray_features(_lib.ptr(packed), _lib.ptr(dirs), R, _lib.ptr(app), rows, _lib.ptr(feat), s),
                "nerf_ray_features")
     _lib.check(lib.nerf_mlp_forward(_lib.ptr(packed), _lib.ptr(origins), _lib.ptr(dirs), _lib.ptr(z_vals), R, N,
-                                    _lib.ptr(feat), _lib.ptr(rgb), _lib.ptr(sigma), s), "nerf_mlp_forward")
+                                    _lib.ptr(feat), _lib.ptr(rgb), _lib.ptr(sigma), None, 0, s), "nerf_mlp_forward")
     return rgb.reshape(*lead, 3).to(out_device), sigma.reshape(*lead, 1).to(out_device)

@@ -13,8 +13,12 @@ and ``background_color``.  Keyword-only extras:
                       draw (B,Nf) — the reference's torch.rand draws (ray_utils.py:80,119).
   seed                key of the in-kernel RNG when no uniforms are given (drawn from the
                       torch CPU generator by default).
-  timing              optional list; when given, (start, end) torch.cuda.Event pairs are
-                      appended around each fused-MLP launch (bench.py's roofline leg).
+  timing              optional list; when given, the path runs stage by stage and appends
+                      (start, end, samples) per fused-MLP launch, the events recorded around
+                      the launch on this stream (bench.py's roofline leg).
+  staged, reuse_coarse  staged=True runs the per-stage entry points instead of the single
+                      nerf_render_rays call; reuse_coarse=False (staged only) re-evaluates the
+                      coarse samples in the fine pass — bit-identical, for the tests.
 ``render_rays`` is the same function (the north-star name).
 """
 import torch
@@ -42,7 +46,7 @@ def packed_for(model):
 
 def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, appearance_embedding=None,
                   background_color=None, perturb=True, *, hierarchical=False, t_rand=None, u_rand=None,
-                  seed=None, timing=None):
+                  seed=None, timing=None, staged=False, reuse_coarse=True):
     dev = _lib.device()
     lib = _lib.load()
     orig_shape = rays_o.shape
@@ -69,7 +73,7 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
     if Nf:
         crgb = torch.empty(B, 3, device=dev)
         cdepth = torch.empty(B, 1, device=dev)
-    if timing is None:
+    if timing is None and not staged:
         ws = torch.empty(lib.nerf_render_workspace_bytes(B, N, Nf), dtype=torch.uint8, device=dev)
         _lib.check(lib.nerf_render_rays(
             _lib.ptr(packed), _lib.ptr(o), _lib.ptr(d), B, float(near), float(far), N, Nf, _lib.ptr(t_vals),
@@ -81,7 +85,8 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
             cw, cz = None, None
     else:
         cw, cz = _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed, app, rows,
-                         rgb_map, depth_map, weights, z_vals, crgb if Nf else None, cdepth if Nf else None, timing)
+                         rgb_map, depth_map, weights, z_vals, crgb if Nf else None, cdepth if Nf else None, timing,
+                         reuse_coarse)
     out = rays_o.device
     if T == 1:   # the reference's per-sample tensors are empty at one sample (render.py:56-58)
         weights = weights[:, :0]
@@ -97,9 +102,11 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
 
 
 def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed, app, rows, rgb_map,
-            depth_map, weights, z_out, crgb, cdepth, timing):
-    """The same kernel sequence as nerf_render_rays, issued stage by stage through the per-stage
-    entry points so each fused-MLP launch can be bracketed by events on this stream."""
+            depth_map, weights, z_out, crgb, cdepth, timing, reuse_coarse=True):
+    """The kernel sequence of nerf_render_rays, issued stage by stage through the per-stage entry
+    points so every fused-MLP launch can be bracketed by events on this stream.  With
+    reuse_coarse=False the fine pass re-evaluates all N+Nf merged samples instead (the reference
+    semantics spelled out; bit-identical results, used by the tests)."""
     dev = o.device
     s = _lib.stream()
     P = _lib.ptr
@@ -111,30 +118,42 @@ def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, 
     feat = torch.empty(B, 256, device=dev)
     _lib.check(lib.nerf_ray_features(P(packed), P(dn), B, P(app), rows, P(feat), s), "nerf_ray_features")
     T = N + Nf
-    rgb = torch.empty(B * T, 3, device=dev)
-    sigma = torch.empty(B * T, device=dev)
 
-    def mlp(zz, n):
+    def mlp(zz, n, rgb, sigma, slot=None):
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-        _lib.check(lib.nerf_mlp_forward(P(packed), P(o), P(dn), P(zz), B, n, P(feat), P(rgb), P(sigma), s),
-                   "nerf_mlp_forward")
+        _lib.check(lib.nerf_mlp_forward(P(packed), P(o), P(dn), P(zz), B, n, P(feat), P(rgb), P(sigma), P(slot),
+                                        T, s), "nerf_mlp_forward")
         ev[1].record()
-        timing.append((ev[0], ev[1], B * n))
+        if timing is not None:
+            timing.append((ev[0], ev[1], B * n))
 
-    mlp(z, N)
+    rgb_c = torch.empty(B * N, 3, device=dev)
+    sigma_c = torch.empty(B * N, device=dev)
+    mlp(z, N, rgb_c, sigma_c)
     if not Nf:
-        _lib.check(lib.nerf_composite(P(rgb), P(sigma), P(z), B, N, P(rgb_map), P(depth_map), P(weights), s),
+        _lib.check(lib.nerf_composite(P(rgb_c), P(sigma_c), P(z), B, N, P(rgb_map), P(depth_map), P(weights), s),
                    "nerf_composite")
         z_out.copy_(z)
         return None, None
     wc = torch.empty(B, N, device=dev)
-    _lib.check(lib.nerf_composite(P(rgb), P(sigma), P(z), B, N, P(crgb), P(cdepth), P(wc), s), "nerf_composite")
-    _lib.check(lib.nerf_sample_importance(P(o), P(dn), P(z), P(wc), B, N, Nf, P(u_lin), P(ur),
-                                          (seed or 0) ^ 0x5DEECE66D, P(z_out), None, s), "nerf_sample_importance")
-    mlp(z_out, T)
-    _lib.check(lib.nerf_composite(P(rgb), P(sigma), P(z_out), B, T, P(rgb_map), P(depth_map), P(weights), s),
-               "nerf_composite")
+    _lib.check(lib.nerf_composite(P(rgb_c), P(sigma_c), P(z), B, N, P(crgb), P(cdepth), P(wc), s), "nerf_composite")
+    rgb_all = torch.empty(B * T, 3, device=dev)
+    sigma_all = torch.empty(B * T, device=dev)
+    key = (seed or 0) ^ 0x5DEECE66D
+    if reuse_coarse:
+        z_fine = torch.empty(B, Nf, device=dev)
+        slot = torch.empty(B, Nf, dtype=torch.int32, device=dev)
+        _lib.check(lib.nerf_sample_importance_merge(P(z), P(wc), P(rgb_c), P(sigma_c), B, N, Nf, P(u_lin), P(ur), key,
+                                                    P(z_out), P(rgb_all), P(sigma_all), P(z_fine), P(slot), s),
+                   "nerf_sample_importance_merge")
+        mlp(z_fine, Nf, rgb_all, sigma_all, slot)
+    else:
+        _lib.check(lib.nerf_sample_importance(P(o), P(dn), P(z), P(wc), B, N, Nf, P(u_lin), P(ur), key, P(z_out),
+                                              None, s), "nerf_sample_importance")
+        mlp(z_out, T, rgb_all, sigma_all)
+    _lib.check(lib.nerf_composite(P(rgb_all), P(sigma_all), P(z_out), B, T, P(rgb_map), P(depth_map), P(weights),
+                                  s), "nerf_composite")
     return wc, z
 
 

@@ -81,6 +81,16 @@ int nerf_sample_importance(const float* rays_o, const float* rays_d, const float
                            const float* u_rand, uint64_t seed, float* z_all, float* pts_all,
                            nerf_stream_t stream);
 
+/* The same resample fused with the coarse-evaluation reuse of the hierarchical pass:
+ * besides z_all it scatters the coarse (rgb_c (B,N,3), sigma_c (B,N)) into their merged
+ * slots of rgb_all (B,N+Nf,3) / sigma_all (B,N+Nf), and emits the fine samples z_fine (B,Nf)
+ * with their merged slots fine_slot (B,Nf), for nerf_mlp_forward(..., out_slot=fine_slot). */
+int nerf_sample_importance_merge(const float* z_vals, const float* weights, const float* rgb_c,
+                                 const float* sigma_c, int64_t B, int N, int Nf,
+                                 const float* u_lin, const float* u_rand, uint64_t seed,
+                                 float* z_all, float* rgb_all, float* sigma_all, float* z_fine,
+                                 int32_t* fine_slot, nerf_stream_t stream);
+
 /* -------------------------------------------------------- R5 packed weights
  * NeRF parameters (src/models.py:58-103) in the MFMA fragment layout of the
  * fused MLP.  params: 24 device pointers in state_dict order
@@ -108,10 +118,11 @@ int nerf_ray_features(const float* packed, const float* dirs, int64_t R, const f
  * With z_vals non-null sample s of ray r sits at pts = origins[r] + dirs[r]*z[r*N+s]
  * (src/ray_utils.py:86); with z_vals null the (R,3) `origins` ARE the points
  * (N must be 1).  ray_feat: (R,256) from nerf_ray_features.  Outputs rgb (M,3),
- * sigma (M) (== (M,1)). */
+ * sigma (M) (== (M,1)); with out_slot (R,N) non-null, sample s of ray r is written at
+ * row r*out_T + out_slot[r*N+s] instead (the scatter of the hierarchical fine pass). */
 int nerf_mlp_forward(const float* packed, const float* origins, const float* dirs,
                      const float* z_vals, int64_t R, int N, const float* ray_feat, float* rgb,
-                     float* sigma, nerf_stream_t stream);
+                     float* sigma, const int32_t* out_slot, int out_T, nerf_stream_t stream);
 
 /* ------------------------------------------------------------- R7 composite
  * Alpha compositing of volume_render (src/render.py:56-80): dists padded with
@@ -125,7 +136,8 @@ int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, in
 /* ------------------------------------------------------------ the whole path
  * volume_render (src/render.py:5-97): normalise dirs, stratified sampling,
  * ray features, fused MLP, composite; with Nf > 0 the H1 hierarchical pass
- * (resample, fused MLP over the N+Nf merged samples, composite).  Nf == 0 is
+ * (resample, fused MLP over the Nf new samples with the N coarse evaluations reused —
+ * bit-identical to evaluating all N+Nf merged samples — composite over N+Nf).  Nf == 0 is
  * the reference's compat mode (its n_importance is ignored, render.py:83-86).
  * Outputs: rgb_map (B,3), depth_map (B) of the final pass; weights_out
  * (B,N+Nf or N) and z_out (same) nullable; coarse_rgb/coarse_depth nullable

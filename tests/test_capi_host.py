@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/nerfmi.h"
-    assert lib.nerf_abi_version() == 1
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -39,7 +39,7 @@ def test_bad_arguments_are_reported_not_launched():
     assert rc == 3
     rc = lib.nerf_sample_importance(None, None, None, None, 4, 300, 128, None, None, 0, None, None, None)
     assert rc == 3
-    rc = lib.nerf_mlp_forward(None, None, None, None, 4, 2, None, None, None, None)
+    rc = lib.nerf_mlp_forward(None, None, None, None, 4, 2, None, None, None, None, 0, None)
     assert rc == 1 and b"N must be 1" in lib.nerf_last_error()
     assert lib.nerf_render_workspace_bytes(0, 64, 128) == 0 or lib.nerf_render_workspace_bytes(0, 64, 128) >= 0
     assert lib.nerf_render_workspace_bytes(-1, 64, 0) == 0

@@ -307,3 +307,24 @@ def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_met
     assert float(psnr) > 80, float(psnr)
     assert float(inside) >= 0.995, float(inside)
     assert float((err / r_ref.abs()).max()) < 1e-3
+
+
+def test_coarse_reuse_is_bit_identical(nerfmi_mod, model, golden, app_vec):
+    """The fine pass evaluates only the Nf new samples and reuses the coarse evaluations; that must
+    give exactly the bits of re-evaluating all N+Nf merged samples (the reference's formulation)."""
+    o, d = crop(golden, "hotdog")
+    torch.manual_seed(14)
+    u = torch.rand(o.shape[0], 128)
+    t = torch.rand(o.shape[0], 64)
+    kw = dict(appearance_embedding=app_vec.cuda(), perturb=True, hierarchical=True, t_rand=t, u_rand=u)
+    a = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, **kw)                  # C, reuse
+    b = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, staged=True, **kw)     # staged, reuse
+    c = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, staged=True, reuse_coarse=False, **kw)
+    for x in (b, c):
+        assert torch.equal(a[0], x[0]) and torch.equal(a[1], x[1])
+        assert torch.equal(a[2]["weights"], x[2]["weights"]) and torch.equal(a[2]["z_vals"], x[2]["z_vals"])
+    # in-kernel RNG path (no explicit uniforms): C and staged agree too
+    kw = dict(appearance_embedding=app_vec.cuda(), perturb=True, hierarchical=True, seed=5)
+    a = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, **kw)
+    c = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, staged=True, reuse_coarse=False, **kw)
+    assert torch.equal(a[0], c[0]) and torch.equal(a[1], c[1])
