@@ -56,21 +56,38 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// One dense layer (or, INIT=false, a further K-slice accumulated onto `out`): NT output tiles of 32 neurons, KS_ACT activation k-steps read from `in`
-// registers and KS_PE positional-encoding k-steps read from `pe`.  Weight fragments stream
-// from L2 through a register ring DEPTH blocks deep (1 KiB per block per wave).
-template <int NT, int KS_ACT, int KS_PE, bool INIT, bool RELU>
+#ifndef NERF_MLP_SPLIT
+#define NERF_MLP_SPLIT 2      // independent accumulation chains per output tile
+#endif
+#ifndef NERF_MLP_DEPTH
+#define NERF_MLP_DEPTH 8      // weight-fragment blocks in flight per wave
+#endif
+
+// One dense layer: NT output tiles of 32 neurons, KS_ACT activation k-steps read from the `in`
+// registers and KS_PE positional-encoding k-steps read from `pe`.  BIAS: the tile starts at zero
+// and the per-neuron vector `init` (a bias, or the per-ray colour feature) is added after the
+// last k-step — its loads are issued at the tile's first k-step and land long before they are
+// needed.  Without BIAS the layer is a further K-slice accumulated onto `out` (the skip layer's
+// PE inputs).  Each tile is accumulated in SPLIT chains taking alternate k-steps, summed at the
+// end: consecutive MFMAs are independent, and each chain is SPLIT times shorter (less rounding
+// growth than one K-long chain).  Weight fragments stream from L2 through a register ring
+// DEPTH blocks deep (1 KiB per block per wave).
+template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU>
 __device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ init,
                                       const f32x16 (&in)[8], const float (&pe)[kPeSteps],
                                       f32x16 (&out)[8], int lane) {
   constexpr int KS = KS_ACT + KS_PE;
   constexpr int KSQ = KS / 4;
   constexpr int G = NT * KSQ;
-  constexpr int DEPTH = 8;
+  constexpr int DEPTH = NERF_MLP_DEPTH;
+  constexpr int SPLIT = NERF_MLP_SPLIT;
   static_assert(G >= DEPTH, "layer too small for the prefetch ring");
+  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "SPLIT must divide a k-quad");
   const int h = lane >> 5;
   const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
   f32x4 ring[DEPTH];
+  f32x16 part[SPLIT];
+  f32x4 bv[4];
   static_for<DEPTH>([&](auto pc) __attribute__((always_inline)) {
     ring[pc.value] = wf[pc.value * 64];
   });
@@ -79,16 +96,38 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
     constexpr int nt = g / KSQ, kq = g % KSQ;
     const f32x4 w = ring[g % DEPTH];
     if constexpr (g + DEPTH < G) ring[g % DEPTH] = wf[(g + DEPTH) * 64];
-    if constexpr (INIT && kq == 0) out[nt] = load_rows(init, nt, h);
+    if constexpr (kq == 0) {
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
+        part[0] = f32x16{};
+      } else {
+        part[0] = out[nt];
+      }
+#pragma unroll
+      for (int c = 1; c < SPLIT; ++c) part[c] = f32x16{};
+    }
     static_for<4>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       constexpr int ks = 4 * kq + j;
       float b;
       if constexpr (ks < KS_ACT) b = in[ks >> 4][ks & 15];
       else b = pe[ks - KS_ACT];
-      out[nt] = mfma32(w[j], b, out[nt]);
+      part[j % SPLIT] = mfma32(w[j], b, part[j % SPLIT]);
     });
-    if constexpr (RELU && kq == KSQ - 1) relu16(out[nt]);
+    if constexpr (kq == KSQ - 1) {
+      f32x16 acc = part[0];
+#pragma unroll
+      for (int c = 1; c < SPLIT; ++c) acc += part[c];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[4 * q + e] += bv[q][e];
+      }
+      if constexpr (RELU) relu16(acc);
+      out[nt] = acc;
+    }
     // keep the ring's issue order: without this the scheduler hoists the whole layer's
     // weight loads and spills
     __builtin_amdgcn_sched_barrier(0);
@@ -118,7 +157,11 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   }
 
   // Positional encoding in the k order of layout.h::pe_feature: sin(2^i x_c) on lane half 0,
-  // cos on half 1 (models.py:36-44; 2^i x is exact, sin/cos fully range-reduced).
+  // cos on half 1 (models.py:36-44; 2^i x is exact, sin/cos fully range-reduced).  Layer 0
+  // reads it from registers; the skip layer reads it back from this wave's LDS slice
+  // (32 floats x 64 lanes), so it does not occupy 32 registers through layers 1..3.
+  __shared__ float pe_lds[4][kPeSteps][64];
+  float (*pe_mine)[64] = pe_lds[threadIdx.x >> 6];
   float pe[kPeSteps];
 #pragma unroll
   for (int i = 0; i < kPosLevels; ++i) {
@@ -131,6 +174,8 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   }
   pe[30] = h ? x[1] : x[0];
   pe[31] = h ? 0.0f : x[2];
+#pragma unroll
+  for (int p = 0; p < kPeSteps; ++p) pe_mine[p][lane] = pe[p];
 
   const float* bias = packed + kOffBias;
   const float* wtrunk = packed + frag_offset(1);                 // layers 1..7, frag_floats(1) apart
@@ -145,7 +190,12 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
                                        B, lane);
     dense<8, kActSteps, 0, true, false>(wtrunk + (size_t)(m2 - 1) * frag_floats(1), bias + m2 * kHidden, B, pe,
                                         A, lane);
-    if (m2 == kSkipLayer) dense<8, 0, kPeSteps, false, false>(packed + frag_offset(kSkipPeMat), bias, A, pe, A, lane);
+    if (m2 == kSkipLayer) {
+      float pe2[kPeSteps];
+#pragma unroll
+      for (int q = 0; q < kPeSteps; ++q) pe2[q] = pe_mine[q][lane];
+      dense<8, 0, kPeSteps, false, false>(packed + frag_offset(kSkipPeMat), bias, A, pe2, A, lane);
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) relu16(A[t]);
   }
