@@ -71,31 +71,134 @@ __device__ __forceinline__ void static_for(F&& f) {
 // PE inputs).  Each tile is accumulated in SPLIT chains taking alternate k-steps, summed at the
 // end: consecutive MFMAs are independent, and each chain is SPLIT times shorter (less rounding
 // growth than one K-long chain).  Weight fragments stream from L2 through a register ring
-// DEPTH blocks deep (1 KiB per block per wave).
+// DEPTH blocks deep (1 KiB per block per wave) that runs across layers: on entry `ring` holds
+// this matrix's first DEPTH blocks, and the last DEPTH steps load the first DEPTH blocks of
+// `next` (the last matrix passes any valid fragment array and the loads go unused), so no
+// layer starts on an L2 round trip.
+constexpr int kDepth = NERF_MLP_DEPTH;
+
+__device__ __forceinline__ void ring_fill(f32x4 (&ring)[kDepth], const float* __restrict__ wmat, int lane) {
+  const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
+#pragma unroll
+  for (int p = 0; p < kDepth; ++p) ring[p] = wf[p * 64];
+}
+
+#ifndef NERF_MLP_OVERLAP
+#define NERF_MLP_OVERLAP 0   // 1: overlapped epilogues (spills at this register budget)
+#endif
+
+#if NERF_MLP_OVERLAP
+// Tile epilogues overlapped with the next tile's MFMAs.  Tile nt accumulates in acc[nt & 1]
+// (one chain: the 32x32x2 f32 MFMA's dependent latency equals its issue interval); its
+// epilogue (+ bias, ReLU, copy to `out`) runs inside the first two k-quads of tile nt+1,
+// interleaved one MFMA to ~10 VALU by sched_group_barrier so it issues in the MFMA shadow
+// instead of draining the matrix pipe.  The bias of tile nt is loaded at its second k-quad
+// (after tile nt-1's epilogue consumed the previous one).  The last tile's epilogue stays at
+// the end of the layer.
 template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU>
-__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ init,
+__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next,
+                                      f32x4 (&ring)[kDepth], const float* __restrict__ init,
                                       const f32x16 (&in)[8], const float (&pe)[kPeSteps],
                                       f32x16 (&out)[8], int lane) {
   constexpr int KS = KS_ACT + KS_PE;
   constexpr int KSQ = KS / 4;
   constexpr int G = NT * KSQ;
-  constexpr int DEPTH = NERF_MLP_DEPTH;
-  constexpr int SPLIT = NERF_MLP_SPLIT;
-  static_assert(G >= DEPTH, "layer too small for the prefetch ring");
-  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "SPLIT must divide a k-quad");
+  constexpr int DEPTH = kDepth;
+  static_assert(G >= DEPTH && G % DEPTH == 0, "the ring hands over whole DEPTH-block windows");
+  static_assert(KSQ >= 2, "the epilogue spans two k-quads");
   const int h = lane >> 5;
   const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
-  f32x4 ring[DEPTH];
-  f32x16 part[SPLIT];
+  const f32x4* __restrict__ nf = reinterpret_cast<const f32x4*>(next) + lane;
+  f32x16 acc[2];
   f32x4 bv[4];
-  static_for<DEPTH>([&](auto pc) __attribute__((always_inline)) {
-    ring[pc.value] = wf[pc.value * 64];
-  });
+  auto epilogue = [&](auto ntc) __attribute__((always_inline)) {
+    constexpr int t = decltype(ntc)::value;
+    f32x16 a = acc[t & 1];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[4 * q + e] += bv[q][e];
+    }
+    if constexpr (RELU) relu16(a);
+    out[t] = a;
+  };
   static_for<G>([&](auto gc) __attribute__((always_inline)) {
     constexpr int g = decltype(gc)::value;
     constexpr int nt = g / KSQ, kq = g % KSQ;
     const f32x4 w = ring[g % DEPTH];
-    if constexpr (g + DEPTH < G) ring[g % DEPTH] = wf[(g + DEPTH) * 64];
+#ifndef NERF_MLP_NOLOAD
+    if constexpr (g + DEPTH < G) {
+      ring[g % DEPTH] = wf[(g + DEPTH) * 64];
+    } else {
+      ring[g % DEPTH] = nf[(g + DEPTH - G) * 64];
+    }
+#else   // timing-only build: the weight stream removed (wrong results)
+    asm volatile("" : "+v"(ring[g % DEPTH]));
+#endif
+    if constexpr (kq == 0) {
+      if constexpr (BIAS) acc[nt & 1] = f32x16{};
+      else acc[nt & 1] = out[nt];
+    }
+    static_for<4>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int ks = 4 * kq + j;
+      float b;
+      if constexpr (ks < KS_ACT) b = in[ks >> 4][ks & 15];
+      else b = pe[ks - KS_ACT];
+      acc[nt & 1] = mfma32(w[j], b, acc[nt & 1]);
+    });
+    if constexpr (kq == 0 && nt > 0) epilogue(std::integral_constant<int, nt - 1>{});
+    if constexpr (BIAS && kq == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
+    }
+    if constexpr (kq == 1 && nt > 0) {
+      // region = k-quads 0 and 1 of tile nt: 8 MFMAs with the previous tile's epilogue between them
+      static_for<8>([&](auto) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // up to 10 VALU
+      });
+    }
+    if constexpr (kq != 0 || nt == 0) {
+      // keep the ring's issue order: without this the scheduler hoists the whole layer's
+      // weight loads and spills
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+  epilogue(std::integral_constant<int, NT - 1>{});
+}
+#else
+template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU>
+__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next,
+                                      f32x4 (&ring)[kDepth], const float* __restrict__ init,
+                                      const f32x16 (&in)[8], const float (&pe)[kPeSteps],
+                                      f32x16 (&out)[8], int lane) {
+  constexpr int KS = KS_ACT + KS_PE;
+  constexpr int KSQ = KS / 4;
+  constexpr int G = NT * KSQ;
+  constexpr int DEPTH = kDepth;
+  constexpr int SPLIT = NERF_MLP_SPLIT;
+  static_assert(G >= DEPTH && G % DEPTH == 0, "the ring hands over whole DEPTH-block windows");
+  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "SPLIT must divide a k-quad");
+  const int h = lane >> 5;
+  const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
+  const f32x4* __restrict__ nf = reinterpret_cast<const f32x4*>(next) + lane;
+  f32x16 part[SPLIT];
+  f32x4 bv[4];
+  static_for<G>([&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value;
+    constexpr int nt = g / KSQ, kq = g % KSQ;
+    const f32x4 w = ring[g % DEPTH];
+#ifndef NERF_MLP_NOLOAD
+    if constexpr (g + DEPTH < G) {
+      ring[g % DEPTH] = wf[(g + DEPTH) * 64];
+    } else {
+      ring[g % DEPTH] = nf[(g + DEPTH - G) * 64];
+    }
+#else   // timing-only build: the weight stream removed (wrong results)
+    asm volatile("" : "+v"(ring[g % DEPTH]));
+#endif
     if constexpr (kq == 0) {
       if constexpr (BIAS) {
 #pragma unroll
@@ -133,6 +236,8 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
     __builtin_amdgcn_sched_barrier(0);
   });
 }
+
+#endif  // NERF_MLP_OVERLAP
 
 __global__ void __launch_bounds__(256, 1)
 mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
@@ -179,28 +284,31 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 
   const float* bias = packed + kOffBias;
   const float* wtrunk = packed + frag_offset(1);                 // layers 1..7, frag_floats(1) apart
+  auto wlayer = [&](int m) { return wtrunk + (size_t)(m - 1) * frag_floats(1); };
+  const float* wskip = packed + frag_offset(kSkipPeMat);
+  f32x4 ring[kDepth];
+  ring_fill(ring, packed + frag_offset(0), lane);
   f32x16 A[8], B[8];
   // layer 0: PE(63) -> 256
-  dense<8, 0, kPeSteps, true, true>(packed + frag_offset(0), bias, A, pe, A, lane);
+  dense<8, 0, kPeSteps, true, true>(packed + frag_offset(0), wlayer(1), ring, bias, A, pe, A, lane);
   // layers 1..6 as three A->B->A pairs; the skip layer 4 adds its PE slice before its ReLU.
 #pragma unroll 1
   for (int p = 0; p < 3; ++p) {
     const int m1 = 1 + 2 * p, m2 = 2 + 2 * p;
-    dense<8, kActSteps, 0, true, true>(wtrunk + (size_t)(m1 - 1) * frag_floats(1), bias + m1 * kHidden, A, pe,
-                                       B, lane);
-    dense<8, kActSteps, 0, true, false>(wtrunk + (size_t)(m2 - 1) * frag_floats(1), bias + m2 * kHidden, B, pe,
-                                        A, lane);
+    dense<8, kActSteps, 0, true, true>(wlayer(m1), wlayer(m2), ring, bias + m1 * kHidden, A, pe, B, lane);
+    dense<8, kActSteps, 0, true, false>(wlayer(m2), m2 == kSkipLayer ? wskip : wlayer(m2 + 1), ring,
+                                        bias + m2 * kHidden, B, pe, A, lane);
     if (m2 == kSkipLayer) {
       float pe2[kPeSteps];
 #pragma unroll
       for (int q = 0; q < kPeSteps; ++q) pe2[q] = pe_mine[q][lane];
-      dense<8, 0, kPeSteps, false, false>(packed + frag_offset(kSkipPeMat), bias, A, pe2, A, lane);
+      dense<8, 0, kPeSteps, false, false>(wskip, wlayer(m2 + 1), ring, bias, A, pe2, A, lane);
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) relu16(A[t]);
   }
   // layer 7: A -> B
-  dense<8, kActSteps, 0, true, true>(wtrunk + 6 * frag_floats(1), bias + 7 * kHidden, A, pe, B, lane);
+  dense<8, kActSteps, 0, true, true>(wlayer(7), packed + frag_offset(8), ring, bias + 7 * kHidden, A, pe, B, lane);
 
   // density head: sigma = ReLU(density_head(h)) (models.py:137-138), h = B.
   const float* ws = packed + kOffSigmaW;
@@ -218,7 +326,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   // colour branch: h_dir = ReLU(W_dh h + [b_dir + W_dd PE(d)]) + appearance (models.py:141-156),
   // the bracket and the appearance part precomputed per ray in `feat`.
   const float* fr = feat + r * kRayFeat;
-  dense<4, kActSteps, 0, true, true>(packed + frag_offset(8), fr, B, pe, A, lane);
+  dense<4, kActSteps, 0, true, true>(packed + frag_offset(8), packed, ring, fr, B, pe, A, lane);
   float pr[3] = {0.0f, 0.0f, 0.0f};
   const float* wr = packed + kOffRgbW;
 #pragma unroll
