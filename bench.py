@@ -4,23 +4,32 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One step = render one 800x800 frame (640,000 rays) per GPU: get_rays -> render_rays
-(hierarchical H1: coarse 64, inverse-CDF 128, fine pass over the 192 merged samples) with
-in-kernel stratified / inverse-CDF RNG, on a random-init NeRF of the reference architecture
-(torch.manual_seed(0); NeRF(Config())).  With N > 1 GPUs each rank renders its own frame of
-the run.py circle path (rank r = frame r: weak scaling, 640,000 rays per GPU) and the
-frames are reassembled on every rank with one RCCL all-gather of [r,g,b,depth] per ray.
+(hierarchical H1: coarse 64, inverse-CDF 128, fine composite over the 192 merged samples, the
+64 coarse evaluations reused bit-identically so the fine MLP evaluates 128) with in-kernel
+stratified / inverse-CDF RNG, on a random-init NeRF of the reference architecture
+(torch.manual_seed(0); NeRF(Config())).  The rays of N frames of the run.py circle
+path are sharded contiguously over the N ranks (frames.py: rank r renders frame r, weak
+scaling, 640,000 rays per GPU) and reassembled on every rank with one RCCL all-gather of
+[r,g,b,depth] per ray.
 Rank 0 prints one JSON line.  value = rays of all ranks / max-over-ranks wall time.
 
 roofline: the dominant kernel is the fused PE->MLP kernel (mlp_kernel).  Its algorithmic
 work is 1,048,832 FLOP per evaluated sample; each step launches it
-twice (B*64 and B*192 samples).  achieved = algorithmic FLOP / kernel time, the time
+twice (B*64 and B*128 samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, the time
 measured with HIP events around every launch inside the timed steps (on the stream it runs
 on); peak = the fp32 MFMA dense peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
 cpu_baseline: the oracle (PyTorch-CPU restatement, oracle/nerf_oracle.py) timed on a
-bounded sample of the same workload on this host's cores (rank 0, N=1 only).
+bounded sample of the same workload on this host's cores (rank 0, N=1 only); the GPU renders
+the same rays with the same uniforms and the line reports the PSNR of its rgb against the
+oracle's (the metric's "PSNR vs reference").
+traffic: HBM bytes per MLP launch from the rocprofv3 PMC passes of scripts/profile_pmc.sh
+(FETCH_SIZE doubled per MI355X_MICROARCH.md + WRITE_SIZE), read from the newest
+profiles/r*_pmc_summary.json when present (PMC counters cannot be read inside this process).
 """
 import argparse
+import glob
 import json
+import math
 import os
 import sys
 import time
@@ -48,8 +57,9 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(target_s):
-    """Oracle H1 render of a centre block of the same frame on the host cores."""
+def cpu_baseline(target_s, gpu_render=None):
+    """Oracle H1 render of a centre block of the same frame on the host cores; with gpu_render,
+    the PSNR of the GPU's rgb on the same rays and uniforms against the oracle's."""
     from oracle import nerf_oracle as O
     from nerfmi import cameras
     state = O.random_state(0)
@@ -64,20 +74,34 @@ def cpu_baseline(target_s):
         torch.manual_seed(2)
         t_rand = torch.rand(n, N_COARSE)
         u_rand = torch.rand(n, N_FINE)
+        args = (o[sl].contiguous(), d[sl].contiguous())
         t0 = time.perf_counter()
-        O.render_rays_h1(state, o[sl].contiguous(), d[sl].contiguous(), 2.0, 6.0, N_COARSE, N_FINE, app,
-                         t_rand, u_rand)
-        return time.perf_counter() - t0
+        rgb, _, _ = O.render_rays_h1(state, *args, 2.0, 6.0, N_COARSE, N_FINE, app, t_rand, u_rand)
+        return time.perf_counter() - t0, args, t_rand, u_rand, rgb
 
     n = 512
-    dt = run(n)
+    dt = run(n)[0]
     n = int(min(65536, max(n, n * target_s / max(dt, 1e-3))))
     n = max(512, (n // 512) * 512)
-    dt = run(n)
-    return {"value": n / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} contiguous rays at the centre of the 800x800 chair frame 0, hierarchical "
-                      f"{N_COARSE}+{N_FINE} (H1), perturbed, oracle/nerf_oracle.py on PyTorch-CPU fp32, "
-                      f"{dt:.1f} s"}
+    dt, rays, t_rand, u_rand, rgb_ref = run(n)
+    out = {"value": n / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+           "sample": f"{n} contiguous rays at the centre of the 800x800 chair frame 0, hierarchical "
+                     f"{N_COARSE}+{N_FINE} (H1), perturbed, oracle/nerf_oracle.py on PyTorch-CPU fp32, {dt:.1f} s"}
+    psnr = None
+    if gpu_render is not None:
+        rgb = gpu_render(*rays, app, t_rand, u_rand).cpu()
+        mse = float(((rgb - rgb_ref) ** 2).mean())
+        psnr = float("inf") if mse == 0 else -10.0 * math.log10(mse)
+    return out, psnr
+
+
+def pmc_traffic():
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        js = json.load(f)
+    return js.get("mlp_hbm_bytes_per_launch"), os.path.relpath(paths[-1], REPO)
 
 
 def main():
@@ -89,7 +113,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import nerfmi
-    from nerfmi import cameras
+    from nerfmi import cameras, frames
 
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
@@ -97,17 +121,14 @@ def main():
     torch.manual_seed(1)
     app = torch.randn(100, 32)[0].to(dev)
     focal = cameras.synthetic_focal(W)
-    c2w = cameras.frame_c2w(args.scene, "circle", frame=rank % 120, num_frames=120).to(dev)
+    # one frame of the run.py circle path per rank: world x 640,000 rays per step, ray-sharded
+    poses = [cameras.frame_c2w(args.scene, "circle", frame=k % 120, num_frames=120) for k in range(world)]
     B = H * W
-    frames = torch.empty(world, B, 4, device=dev) if world > 1 else None
 
     def step(i, timing=None):
-        o, d = nerfmi.get_rays(H, W, focal, c2w)
-        rgb, depth, _ = nerfmi.render_rays(model, o.reshape(-1, 3), d.reshape(-1, 3), 2.0, 6.0, N_COARSE, N_FINE,
-                                           appearance_embedding=app, perturb=True, hierarchical=True,
-                                           seed=1000 * rank + i, timing=timing)
-        if world > 1:
-            dist.all_gather_into_tensor(frames.view(-1), torch.cat([rgb, depth], dim=1).reshape(-1))
+        rgb, depth = frames.render_path_frames(model, poses, H, W, focal, 2.0, 6.0, N_COARSE, N_FINE,
+                                               appearance_embedding=app, perturb=True, hierarchical=True, seed=i,
+                                               timing=timing)
         return rgb
 
     for i in range(args.warmup):
@@ -132,8 +153,13 @@ def main():
     mlp_ms = sum(a.elapsed_time(b) for a, b, _ in timing)
     mlp_samples = sum(n for _, _, n in timing)
     achieved = mlp_samples * FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12
+    per_kind = {}
+    for a, b, n in timing:
+        k = "coarse" if n == B * N_COARSE else "fine"
+        per_kind.setdefault(k, []).append(a.elapsed_time(b))
     if rank == 0:
         total_rays = B * world * args.steps
+        traffic, traffic_src = pmc_traffic()
         line = {
             "metric": "rays/sec at 800x800, 64 coarse + 128 fine samples",
             "value": total_rays / elapsed,
@@ -146,21 +172,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic: run.py circle-path pose per rank, random-init NeRF (torch.manual_seed(0)), "
-                    "no dataset/checkpoint in the environment",
+            "data": "synthetic: run.py circle-path poses (one frame per rank), random-init NeRF "
+                    "(torch.manual_seed(0); NeRF(Config())), no dataset/checkpoint in the environment",
             "config": {"workload": f"{args.scene} 800x800 frame per GPU, hierarchical {N_COARSE} coarse + "
-                                   f"{N_FINE} fine (H1, fine pass over 192 merged samples), perturb=True",
+                                   f"{N_FINE} fine (H1; fine composite over 192 merged samples, coarse "
+                                   f"evaluations reused), perturb=True",
                        "rays_per_gpu_per_step": B, "n_coarse": N_COARSE, "n_fine": N_FINE,
+                       "mlp_evals_per_ray": N_COARSE + N_FINE,
                        "parallelism": f"ray-shard x{world} (one frame per GPU) + RCCL all-gather"},
-            "roofline": {"bound": "mfma", "kernel": "mlp_kernel", "achieved": achieved,
+            "roofline": {"bound": "mfma", "kernel": "nerf::mlp_kernel", "achieved": achieved,
                          "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS,
-                         "traffic": None, "launches": len(timing),
-                         "avg_launch_ms": mlp_ms / max(len(timing), 1),
+                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "launches": len(timing), "avg_launch_ms": mlp_ms / max(len(timing), 1),
+                         "avg_launch_ms_by_pass": {k: sum(v) / len(v) for k, v in per_kind.items()},
                          "flop_per_sample": FLOP_PER_SAMPLE},
             "cpu_baseline": None,
+            "psnr_vs_reference_db": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            def gpu_render(o, d, a, t_rand, u_rand):
+                rgb, _, _ = nerfmi.render_rays(model, o.to(dev), d.to(dev), 2.0, 6.0, N_COARSE, N_FINE,
+                                               appearance_embedding=a.to(dev), perturb=True, hierarchical=True,
+                                               t_rand=t_rand, u_rand=u_rand)
+                return rgb
+            line["cpu_baseline"], line["psnr_vs_reference_db"] = cpu_baseline(args.cpu_seconds, gpu_render)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -33,16 +33,18 @@ def draw_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
-def get_rays(height, width, focal_length, c2w):
+def get_rays(height, width, focal_length, c2w, *, rows=None):
     """origins (H,W,3) — a 0-stride expand of c2w[:3,3] as in the reference (:48) — and unit
-    directions (H,W,3) on c2w's device."""
+    directions (H,W,3) on c2w's device.  rows=(row0, nrows) generates only those image rows
+    ((nrows,W,3) outputs; the frame sharding of frames.py)."""
     if c2w.shape[-1] != 4 or c2w.dim() != 2 or c2w.shape[0] not in (3, 4):
         raise ValueError(f"get_rays: c2w must be (3,4) or (4,4), got {tuple(c2w.shape)}")
     dev = _lib.device()
+    row0, nrows = (0, height) if rows is None else (int(rows[0]), int(rows[1]))
     m = c2w[:3, :4].detach().to("cpu", torch.float32).contiguous()
     host = (ctypes.c_float * 12)(*m.flatten().tolist())
-    d = torch.empty(height, width, 3, device=dev)
-    _lib.check(_lib.load().nerf_get_rays(height, width, float(focal_length), host, 0, height, None, _lib.ptr(d),
+    d = torch.empty(nrows, width, 3, device=dev)
+    _lib.check(_lib.load().nerf_get_rays(height, width, float(focal_length), host, row0, nrows, None, _lib.ptr(d),
                                          _lib.stream()), "nerf_get_rays")
     d = d.to(c2w.device)
     return c2w[..., :3, 3].to(torch.float32).expand(d.shape), d

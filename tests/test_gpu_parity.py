@@ -328,3 +328,21 @@ def test_coarse_reuse_is_bit_identical(nerfmi_mod, model, golden, app_vec):
     a = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, **kw)
     c = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, 64, 128, staged=True, reuse_coarse=False, **kw)
     assert torch.equal(a[0], c[0]) and torch.equal(a[1], c[1])
+
+
+def test_render_path_frames_single_rank(nerfmi_mod, model, app_vec):
+    """frames.render_path_frames on one rank equals rendering each frame directly (ray order,
+    row-shard ray generation, reassembly)."""
+    from nerfmi import cameras, frames
+    poses = [cameras.frame_c2w("hotdog", "circle", k, 120) for k in (0, 7)]
+    H, W, f = 40, 56, cameras.synthetic_focal(56)
+    rgb, depth = frames.render_path_frames(model, poses, H, W, f, 2.0, 6.0, 64, 0, appearance_embedding=app_vec,
+                                           perturb=False)
+    assert rgb.shape == (2, H, W, 3) and depth.shape == (2, H, W)
+    for k, c2w in enumerate(poses):
+        o, d = nerfmi_mod.get_rays(H, W, f, c2w.cuda())
+        r, dd, _ = nerfmi_mod.render_rays(model, o.reshape(-1, 3), d.reshape(-1, 3), 2.0, 6.0, 64, 0,
+                                          appearance_embedding=app_vec, perturb=False)
+        assert torch.equal(rgb[k].reshape(-1, 3), r) and torch.equal(depth[k].reshape(-1), dd[:, 0])
+        o2, d2 = nerfmi_mod.get_rays(H, W, f, c2w.cuda(), rows=(5, 9))
+        assert torch.equal(d2, d[5:14])
