@@ -59,6 +59,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 #ifndef NERF_MLP_SPLIT
 #define NERF_MLP_SPLIT 2      // independent accumulation chains per output tile
 #endif
+#ifndef NERF_MLP_WAVES
+#define NERF_MLP_WAVES 4      // waves per workgroup (each wave is independent: no barriers, own LDS slice)
+#endif
 #ifndef NERF_MLP_DEPTH
 #define NERF_MLP_DEPTH 8      // weight-fragment blocks in flight per wave
 #endif
@@ -89,13 +92,16 @@ __device__ __forceinline__ void ring_fill(f32x4 (&ring)[kDepth], const float* __
 
 #if NERF_MLP_OVERLAP
 // Tile epilogues overlapped with the next tile's MFMAs.  Tile nt accumulates in acc[nt & 1]
-// (one chain: the 32x32x2 f32 MFMA's dependent latency equals its issue interval); its
-// epilogue (+ bias, ReLU, copy to `out`) runs inside the first two k-quads of tile nt+1,
-// interleaved one MFMA to ~10 VALU by sched_group_barrier so it issues in the MFMA shadow
-// instead of draining the matrix pipe.  The bias of tile nt is loaded at its second k-quad
-// (after tile nt-1's epilogue consumed the previous one).  The last tile's epilogue stays at
-// the end of the layer.
-template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU>
+// (one chain: the 32x32x2 f32 MFMA's dependent latency equals its issue interval).  With
+// BIAS (a per-neuron vector shared by all samples) the chain starts with one extra MFMA,
+// A = init[nt*32 + (lane&31)], B = 1 on lane half 0 and 0 on half 1, C = 0, which writes
+// the bias into every column exactly; the epilogue is then just ReLU and the copy to `out`,
+// and it runs inside the first two k-quads of tile nt+1, interleaved one MFMA to ~6 VALU by
+// sched_group_barrier, so it issues in the MFMA shadow instead of draining the matrix pipe.
+// The bias value of tile nt+1 is loaded during tile nt.  PERLANE_INIT (the colour branch's
+// per-ray feature, a different vector per sample) is added by VALU in the epilogue instead.
+// The last tile's epilogue stays at the end of the layer.
+template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU, bool PERLANE_INIT = false>
 __device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next,
                                       f32x4 (&ring)[kDepth], const float* __restrict__ init,
                                       const f32x16 (&in)[8], const float (&pe)[kPeSteps],
@@ -109,12 +115,15 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
   const int h = lane >> 5;
   const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
   const f32x4* __restrict__ nf = reinterpret_cast<const f32x4*>(next) + lane;
+  const float one_h0 = h ? 0.0f : 1.0f;
   f32x16 acc[2];
   f32x4 bv[4];
+  float bnext = 0.0f;
+  if constexpr (BIAS && !PERLANE_INIT) bnext = init[lane & 31];
   auto epilogue = [&](auto ntc) __attribute__((always_inline)) {
     constexpr int t = decltype(ntc)::value;
     f32x16 a = acc[t & 1];
-    if constexpr (BIAS) {
+    if constexpr (PERLANE_INIT) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -137,8 +146,9 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
     asm volatile("" : "+v"(ring[g % DEPTH]));
 #endif
     if constexpr (kq == 0) {
-      if constexpr (BIAS) acc[nt & 1] = f32x16{};
-      else acc[nt & 1] = out[nt];
+      if constexpr (!BIAS) acc[nt & 1] = out[nt];
+      else if constexpr (PERLANE_INIT) acc[nt & 1] = f32x16{};
+      else acc[nt & 1] = mfma32(bnext, one_h0, f32x16{});
     }
     static_for<4>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
@@ -149,15 +159,19 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
       acc[nt & 1] = mfma32(w[j], b, acc[nt & 1]);
     });
     if constexpr (kq == 0 && nt > 0) epilogue(std::integral_constant<int, nt - 1>{});
-    if constexpr (BIAS && kq == 1) {
+    if constexpr (kq == 1 && BIAS) {
+      if constexpr (PERLANE_INIT) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
+        for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
+      } else if constexpr (nt + 1 < NT) {
+        bnext = init[(nt + 1) * 32 + (lane & 31)];
+      }
     }
     if constexpr (kq == 1 && nt > 0) {
-      // region = k-quads 0 and 1 of tile nt: 8 MFMAs with the previous tile's epilogue between them
-      static_for<8>([&](auto) __attribute__((always_inline)) {
+      // region = k-quads 0 and 1 of tile nt: 8 (9) MFMAs with the previous tile's epilogue between them
+      static_for<9>([&](auto) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);  // up to 10 VALU
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // up to 6 VALU
       });
     }
     if constexpr (kq != 0 || nt == 0) {
@@ -239,12 +253,12 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
 
 #endif  // NERF_MLP_OVERLAP
 
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(64 * NERF_MLP_WAVES, 1)
 mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
            const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
            float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
   const int lane = threadIdx.x & 63;
-  const int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
+  const int64_t s0 = ((int64_t)blockIdx.x * NERF_MLP_WAVES + (threadIdx.x >> 6)) * 32;
   if (s0 >= M) return;
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
@@ -265,7 +279,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   // cos on half 1 (models.py:36-44; 2^i x is exact, sin/cos fully range-reduced).  Layer 0
   // reads it from registers; the skip layer reads it back from this wave's LDS slice
   // (32 floats x 64 lanes), so it does not occupy 32 registers through layers 1..3.
-  __shared__ float pe_lds[4][kPeSteps][64];
+  __shared__ float pe_lds[NERF_MLP_WAVES][kPeSteps][64];
   float (*pe_mine)[64] = pe_lds[threadIdx.x >> 6];
   float pe[kPeSteps];
 #pragma unroll
@@ -273,7 +287,12 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       float sn, cs;
+#ifndef NERF_MLP_NOPE
       sincosf(x[c] * (float)(1 << i), &sn, &cs);
+#else   // timing-only build: PE without the transcendental (wrong results)
+      sn = x[c] * (float)(1 << i);
+      cs = sn + 1.0f;
+#endif
       pe[3 * i + c] = h ? cs : sn;
     }
   }
@@ -326,7 +345,11 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   // colour branch: h_dir = ReLU(W_dh h + [b_dir + W_dd PE(d)]) + appearance (models.py:141-156),
   // the bracket and the appearance part precomputed per ray in `feat`.
   const float* fr = feat + r * kRayFeat;
+#if NERF_MLP_OVERLAP
+  dense<4, kActSteps, 0, true, true, true>(packed + frag_offset(8), packed, ring, fr, B, pe, A, lane);
+#else
   dense<4, kActSteps, 0, true, true>(packed + frag_offset(8), packed, ring, fr, B, pe, A, lane);
+#endif
   float pr[3] = {0.0f, 0.0f, 0.0f};
   const float* wr = packed + kOffRgbW;
 #pragma unroll
@@ -360,8 +383,9 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
                const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
-  const int64_t blocks = (M + 127) / 128;
-  hipLaunchKernelGGL(mlp_kernel, dim3((unsigned)blocks), dim3(256), 0, s, packed, o, d, z, M, N, feat, rgb,
+  constexpr int per_block = 32 * NERF_MLP_WAVES;
+  const int64_t blocks = (M + per_block - 1) / per_block;
+  hipLaunchKernelGGL(mlp_kernel, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M, N, feat, rgb,
                      sigma, out_slot, out_T);
   return check_launch("mlp_kernel");
 }
