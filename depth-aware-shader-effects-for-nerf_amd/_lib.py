@@ -13,6 +13,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG_DIR, "libnerfmi.so")
 
 _c_float_p = ctypes.c_void_p  # device pointers travel as integers
+_V, _I64 = ctypes.c_void_p, ctypes.c_int64
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
@@ -55,10 +56,34 @@ _SIGNATURES = {
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_void_p]),
+    # training (include/nerfmi_train.h)
+    "nerf_packed_transposed_floats": (ctypes.c_size_t, []),
+    "nerf_pack_weights_transposed": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
+    "nerf_pack_weights_transposed_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "nerf_ray_features_train": (ctypes.c_int, [_V, _V, _I64, _V, _I64, _V, _V, _V]),
+    "nerf_mlp_forward_train": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V, _V, _V, _V]),
+    "nerf_composite_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, ctypes.c_int, ctypes.c_float, _V, _V, _V,
+                                               _V]),
+    "nerf_mlp_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _I64, _V, _V]),
+    "nerf_param_grads_workspace_bytes": (ctypes.c_size_t, [_I64]),
+    "nerf_param_grads": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, _V, _I64, _V, ctypes.POINTER(ctypes.c_void_p),
+                                        _V, _V, ctypes.c_size_t, _V]),
+    "nerf_wgrad_workspace_bytes": (ctypes.c_size_t, [_I64, ctypes.c_int, ctypes.c_int]),
+    "nerf_wgrad": (ctypes.c_int, [_V, _I64, ctypes.c_int, _V, _I64, ctypes.c_int, _I64, _I64, _V, _V, ctypes.c_int,
+                                  _V, ctypes.c_size_t, _V]),
+    "nerf_adam": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, _I64, _V]),
+    "nerf_train_workspace_bytes": (ctypes.c_size_t, [_I64, ctypes.c_int]),
+    "nerf_train_forward": (ctypes.c_int, [_V, _V, _V, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_int, _V,
+                                          ctypes.c_int, _V, ctypes.c_uint64, _V, _I64, _V, _V, _V, ctypes.c_size_t,
+                                          _V]),
+    "nerf_train_backward": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _I64,
+                                           ctypes.POINTER(ctypes.c_void_p), _V, _V, _V, ctypes.c_size_t, _V]),
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
-#include "../../include/nerfmi.h"
+#include "../../include/nerfmi_train.h"
 #include "layout.h"
 
 namespace nerf {
@@ -46,10 +46,10 @@ int launch_importance(const float* o, const float* d, const float* z, const floa
                       float* rgb_all, float* sigma_all, float* z_fine, int* fine_slot, hipStream_t s);
 int launch_pack(const float* const* params, float* packed, hipStream_t s);
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
-                        int64_t app_rows, float* feat, hipStream_t s);
+                        int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
                int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
-               hipStream_t s);
+               hipStream_t s, float* save = nullptr, const float* encd = nullptr);
 int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N,
                      float* rgb_map, float* depth, float* weights, hipStream_t s);
 

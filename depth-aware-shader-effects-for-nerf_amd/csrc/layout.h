@@ -107,6 +107,29 @@ NERF_HD inline int frag_source_col(int m, int ks, int lane) {
 }  // namespace nerf
 
 namespace nerf {
+// Training: per-sample activation row saved by the forward pass (nerf_mlp_forward_train),
+// laid out so every weight-gradient input is one contiguous slice:
+//   [h0 | h1 | h2 | h3 | enc_x(64) | h4 | h5 | h6 | h7 | enc_d(32) | r_dir(128) | hd(128)]
+// h_l = ReLU(layer l) (256 each), enc_x = PE_10(x) (63 + a zero), enc_d = PE_4(d) (27 + 5 zeros),
+// r_dir = ReLU(dir_linear(...)), hd = r_dir + appearance feature (the rgb head's input).
+// Layer 4's input [h3, enc_x] and the colour branch's [h7, enc_d] are contiguous
+// (models.py:131, :141).
+constexpr int kSaveEncX = 4 * kHidden;                       // 1024
+NERF_HD constexpr int save_h(int l) { return l < 4 ? l * kHidden : kSaveEncX + 64 + (l - 4) * kHidden; }
+constexpr int kSaveEncD = 1088 + 4 * kHidden;                // 2112
+constexpr int kSaveRDir = kSaveEncD + 32;                    // 2144
+constexpr int kSaveHd = kSaveRDir + kDirHidden;              // 2272
+constexpr int kSaveRow = kSaveHd + kDirHidden;               // 2400 floats per sample
+
+// Per-sample gradient row written by the backward pass (nerf_mlp_backward):
+//   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dhd (128) | dsigma_pre | drgb_pre (3)]
+// dpre_l = d loss / d (pre-activation of trunk layer l), dhd = d loss / d hd.
+constexpr int kGradDir = 8 * kHidden;                        // 2048
+constexpr int kGradHd = kGradDir + kDirHidden;               // 2176
+constexpr int kGradSigma = kGradHd + kDirHidden;             // 2304
+constexpr int kGradRgb = kGradSigma + 1;                     // 2305
+constexpr int kGradRow = 2308;
+
 // Float offset, inside matrix m's fragment array, of element j of lane `lane` in the
 // fragment block (n-tile nt, k-step quad kq): ks = 4*kq + j.
 NERF_HD inline size_t frag_elem(int m, int nt, int kq, int lane, int j) {

@@ -12,6 +12,14 @@
 // registers: the kernel reads only the samples' (o, d, z), the 2 MiB packed weights
 // (L2-resident on every XCD) and writes 16 B per sample.
 //
+// No tile epilogue: each output tile starts with one MFMA that writes its bias into every
+// column (A = bias, B = 1 on lane half 0 / 0 on half 1, C = 0: exact), then accumulates its
+// k-steps in place; ReLU is applied by the CONSUMER when it reads a register as a B operand
+// (one v_max per k-step, shared by the MFMAs of four tiles, issued in the MFMA shadow).  Four
+// output tiles are accumulated together, their MFMAs interleaved, so consecutive MFMAs are
+// independent (one dependent 32x32x2 f32 chain issues at ~90 % of peak, four at ~98 %:
+// profiles/r01_mfma_f32_rate_microbench.log).
+//
 // Bound: MFMA.  1,048,832 algorithmic FLOP per sample; the kernel
 // issues 8,192 MFMAs of 4,096 FLOP per 32 samples (63->64 and 319->320 input padding).
 #include <utility>
@@ -19,6 +27,21 @@
 #include "common.h"
 
 namespace nerf {
+
+#ifdef NERF_MLP_STAMPS   // diagnostic build (scripts/microbench/mlp_stamps.hip): per-wave segment clocks
+__device__ unsigned long long nerf_stamps[65536][12];
+#define NERF_STAMP(i)                                                                       \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long t_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const int64_t w_ = (int64_t)blockIdx.x * NERF_MLP_WAVES + (threadIdx.x >> 6);           \
+    if (w_ < 65536 && (threadIdx.x & 63) == 0) nerf_stamps[w_][i] = t_;                     \
+  } while (0)
+#else
+#define NERF_STAMP(i) do {} while (0)
+#endif
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -39,11 +62,6 @@ __device__ __forceinline__ f32x16 load_rows(const float* __restrict__ v, int nt,
   return out;
 }
 
-__device__ __forceinline__ void relu16(f32x16& v) {
-#pragma unroll
-  for (int e = 0; e < 16; ++e) v[e] = fmaxf(v[e], 0.0f);
-}
-
 // Compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, fully expanded by the
 // front end (the loop unroller gives up on bodies this large and would leave the register
 // arrays runtime-indexed, i.e. in scratch).
@@ -56,9 +74,6 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-#ifndef NERF_MLP_SPLIT
-#define NERF_MLP_SPLIT 2      // independent accumulation chains per output tile
-#endif
 #ifndef NERF_MLP_WAVES
 #define NERF_MLP_WAVES 4      // waves per workgroup (each wave is independent: no barriers, own LDS slice)
 #endif
@@ -66,43 +81,34 @@ __device__ __forceinline__ void static_for(F&& f) {
 #define NERF_MLP_DEPTH 8      // weight-fragment blocks in flight per wave
 #endif
 
-// One dense layer: NT output tiles of 32 neurons, KS_ACT activation k-steps read from the `in`
-// registers and KS_PE positional-encoding k-steps read from `pe`.  BIAS: the tile starts at zero
-// and the per-neuron vector `init` (a bias, or the per-ray colour feature) is added after the
-// last k-step — its loads are issued at the tile's first k-step and land long before they are
-// needed.  Without BIAS the layer is a further K-slice accumulated onto `out` (the skip layer's
-// PE inputs).  Each tile is accumulated in SPLIT chains taking alternate k-steps, summed at the
-// end: consecutive MFMAs are independent, and each chain is SPLIT times shorter (less rounding
-// growth than one K-long chain).  Weight fragments stream from L2 through a register ring
-// DEPTH blocks deep (1 KiB per block per wave) that runs across layers: on entry `ring` holds
-// this matrix's first DEPTH blocks, and the last DEPTH steps load the first DEPTH blocks of
-// `next` (the last matrix passes any valid fragment array and the loads go unused), so no
-// layer starts on an L2 round trip.
+// One dense layer: NT output tiles of 32 neurons in groups of four, KS_ACT activation k-steps
+// read from `in` (ReLU applied on read when RELU_IN) and KS_PE positional-encoding k-steps
+// read from `pe`.  INIT: kBias = bias via one MFMA per tile, kPerLane = a per-sample vector
+// loaded into the accumulator (the colour branch's per-ray feature), kAccum = accumulate onto
+// `out` (the skip layer's PE slice).  Outputs are pre-activations.  Weight fragments stream
+// from L2 through a register ring DEPTH blocks deep (1 KiB per block per wave), in the order
+// they are consumed (tile group, k-quad, tile), and the ring runs across layers: on entry it
+// holds this matrix's first DEPTH blocks of that order, and the last DEPTH loads fetch the
+// first blocks of `next` (the last matrix passes any valid fragment array; those loads go
+// unused; next_ksq is its k-quad count), so no layer starts on an L2 round trip.
 constexpr int kDepth = NERF_MLP_DEPTH;
+enum Init { kBias, kPerLane, kAccum };
 
+// packed block index (layout.h frag_elem / 256) of the g-th block of the consumption order
+template <int NT, int KSQ>
+__device__ __forceinline__ constexpr int stream_block(int g) {
+  return ((g / (4 * KSQ)) * 4 + g % 4) * KSQ + (g / 4) % KSQ;
+}
+
+template <int NT, int KSQ>
 __device__ __forceinline__ void ring_fill(f32x4 (&ring)[kDepth], const float* __restrict__ wmat, int lane) {
   const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
 #pragma unroll
-  for (int p = 0; p < kDepth; ++p) ring[p] = wf[p * 64];
+  for (int p = 0; p < kDepth; ++p) ring[p] = wf[stream_block<NT, KSQ>(p) * 64];
 }
 
-#ifndef NERF_MLP_OVERLAP
-#define NERF_MLP_OVERLAP 0   // 1: overlapped epilogues (spills at this register budget)
-#endif
-
-#if NERF_MLP_OVERLAP
-// Tile epilogues overlapped with the next tile's MFMAs.  Tile nt accumulates in acc[nt & 1]
-// (one chain: the 32x32x2 f32 MFMA's dependent latency equals its issue interval).  With
-// BIAS (a per-neuron vector shared by all samples) the chain starts with one extra MFMA,
-// A = init[nt*32 + (lane&31)], B = 1 on lane half 0 and 0 on half 1, C = 0, which writes
-// the bias into every column exactly; the epilogue is then just ReLU and the copy to `out`,
-// and it runs inside the first two k-quads of tile nt+1, interleaved one MFMA to ~6 VALU by
-// sched_group_barrier, so it issues in the MFMA shadow instead of draining the matrix pipe.
-// The bias value of tile nt+1 is loaded during tile nt.  PERLANE_INIT (the colour branch's
-// per-ray feature, a different vector per sample) is added by VALU in the epilogue instead.
-// The last tile's epilogue stays at the end of the layer.
-template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU, bool PERLANE_INIT = false>
-__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next,
+template <int NT, int KS_ACT, int KS_PE, int INIT, bool RELU_IN>
+__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next, int next_ksq,
                                       f32x4 (&ring)[kDepth], const float* __restrict__ init,
                                       const f32x16 (&in)[8], const float (&pe)[kPeSteps],
                                       f32x16 (&out)[8], int lane) {
@@ -110,159 +116,95 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
   constexpr int KSQ = KS / 4;
   constexpr int G = NT * KSQ;
   constexpr int DEPTH = kDepth;
-  static_assert(G >= DEPTH && G % DEPTH == 0, "the ring hands over whole DEPTH-block windows");
-  static_assert(KSQ >= 2, "the epilogue spans two k-quads");
+  static_assert(NT % 4 == 0 && G >= DEPTH && DEPTH % 4 == 0, "ring/tile-group geometry");
   const int h = lane >> 5;
   const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
   const f32x4* __restrict__ nf = reinterpret_cast<const f32x4*>(next) + lane;
   const float one_h0 = h ? 0.0f : 1.0f;
-  f32x16 acc[2];
-  f32x4 bv[4];
-  float bnext = 0.0f;
-  if constexpr (BIAS && !PERLANE_INIT) bnext = init[lane & 31];
-  auto epilogue = [&](auto ntc) __attribute__((always_inline)) {
-    constexpr int t = decltype(ntc)::value;
-    f32x16 a = acc[t & 1];
-    if constexpr (PERLANE_INIT) {
+  float bias_v[4];
+  if constexpr (INIT == kBias) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[4 * q + e] += bv[q][e];
-    }
-    if constexpr (RELU) relu16(a);
-    out[t] = a;
-  };
-  static_for<G>([&](auto gc) __attribute__((always_inline)) {
-    constexpr int g = decltype(gc)::value;
-    constexpr int nt = g / KSQ, kq = g % KSQ;
-    const f32x4 w = ring[g % DEPTH];
-#ifndef NERF_MLP_NOLOAD
-    if constexpr (g + DEPTH < G) {
-      ring[g % DEPTH] = wf[(g + DEPTH) * 64];
-    } else {
-      ring[g % DEPTH] = nf[(g + DEPTH - G) * 64];
-    }
-#else   // timing-only build: the weight stream removed (wrong results)
-    asm volatile("" : "+v"(ring[g % DEPTH]));
-#endif
+    for (int i = 0; i < 4; ++i) bias_v[i] = init[i * 32 + (lane & 31)];
+  }
+  static_for<G / 4>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int st = decltype(sc)::value;          // one k-quad of one tile group: 4 blocks
+    constexpr int grp = st / KSQ, kq = st % KSQ;
     if constexpr (kq == 0) {
-      if constexpr (!BIAS) acc[nt & 1] = out[nt];
-      else if constexpr (PERLANE_INIT) acc[nt & 1] = f32x16{};
-      else acc[nt & 1] = mfma32(bnext, one_h0, f32x16{});
-    }
-    static_for<4>([&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      constexpr int ks = 4 * kq + j;
-      float b;
-      if constexpr (ks < KS_ACT) b = in[ks >> 4][ks & 15];
-      else b = pe[ks - KS_ACT];
-      acc[nt & 1] = mfma32(w[j], b, acc[nt & 1]);
-    });
-    if constexpr (kq == 0 && nt > 0) epilogue(std::integral_constant<int, nt - 1>{});
-    if constexpr (kq == 1 && BIAS) {
-      if constexpr (PERLANE_INIT) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
-      } else if constexpr (nt + 1 < NT) {
-        bnext = init[(nt + 1) * 32 + (lane & 31)];
-      }
-    }
-    if constexpr (kq == 1 && nt > 0) {
-      // region = k-quads 0 and 1 of tile nt: 8 (9) MFMAs with the previous tile's epilogue between them
-      static_for<9>([&](auto) __attribute__((always_inline)) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // up to 6 VALU
+      static_for<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int t = 4 * grp + i;
+        if constexpr (INIT == kBias) out[t] = mfma32(bias_v[i], one_h0, f32x16{});
+        else if constexpr (INIT == kPerLane) out[t] = load_rows(init, t, h);
       });
-    }
-    if constexpr (kq != 0 || nt == 0) {
-      // keep the ring's issue order: without this the scheduler hoists the whole layer's
-      // weight loads and spills
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  });
-  epilogue(std::integral_constant<int, NT - 1>{});
-}
-#else
-template <int NT, int KS_ACT, int KS_PE, bool BIAS, bool RELU>
-__device__ __forceinline__ void dense(const float* __restrict__ wmat, const float* __restrict__ next,
-                                      f32x4 (&ring)[kDepth], const float* __restrict__ init,
-                                      const f32x16 (&in)[8], const float (&pe)[kPeSteps],
-                                      f32x16 (&out)[8], int lane) {
-  constexpr int KS = KS_ACT + KS_PE;
-  constexpr int KSQ = KS / 4;
-  constexpr int G = NT * KSQ;
-  constexpr int DEPTH = kDepth;
-  constexpr int SPLIT = NERF_MLP_SPLIT;
-  static_assert(G >= DEPTH && G % DEPTH == 0, "the ring hands over whole DEPTH-block windows");
-  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "SPLIT must divide a k-quad");
-  const int h = lane >> 5;
-  const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
-  const f32x4* __restrict__ nf = reinterpret_cast<const f32x4*>(next) + lane;
-  f32x16 part[SPLIT];
-  f32x4 bv[4];
-  static_for<G>([&](auto gc) __attribute__((always_inline)) {
-    constexpr int g = decltype(gc)::value;
-    constexpr int nt = g / KSQ, kq = g % KSQ;
-    const f32x4 w = ring[g % DEPTH];
-#ifndef NERF_MLP_NOLOAD
-    if constexpr (g + DEPTH < G) {
-      ring[g % DEPTH] = wf[(g + DEPTH) * 64];
-    } else {
-      ring[g % DEPTH] = nf[(g + DEPTH - G) * 64];
-    }
-#else   // timing-only build: the weight stream removed (wrong results)
-    asm volatile("" : "+v"(ring[g % DEPTH]));
-#endif
-    if constexpr (kq == 0) {
-      if constexpr (BIAS) {
+      if constexpr (INIT == kBias && grp + 1 < NT / 4) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bv[q] = *reinterpret_cast<const f32x4*>(init + nt * 32 + 8 * q + 4 * h);
-        part[0] = f32x16{};
-      } else {
-        part[0] = out[nt];
+        for (int i = 0; i < 4; ++i) bias_v[i] = init[(4 * (grp + 1) + i) * 32 + (lane & 31)];
       }
-#pragma unroll
-      for (int c = 1; c < SPLIT; ++c) part[c] = f32x16{};
     }
     static_for<4>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       constexpr int ks = 4 * kq + j;
       float b;
-      if constexpr (ks < KS_ACT) b = in[ks >> 4][ks & 15];
-      else b = pe[ks - KS_ACT];
-      part[j % SPLIT] = mfma32(w[j], b, part[j % SPLIT]);
-    });
-    if constexpr (kq == KSQ - 1) {
-      f32x16 acc = part[0];
-#pragma unroll
-      for (int c = 1; c < SPLIT; ++c) acc += part[c];
-      if constexpr (BIAS) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[4 * q + e] += bv[q][e];
+      if constexpr (ks < KS_ACT) {
+        b = in[ks >> 4][ks & 15];
+        if constexpr (RELU_IN) b = fmaxf(b, 0.0f);
+      } else {
+        b = pe[ks - KS_ACT];
       }
-      if constexpr (RELU) relu16(acc);
-      out[nt] = acc;
-    }
-    // keep the ring's issue order: without this the scheduler hoists the whole layer's
-    // weight loads and spills
+      static_for<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        out[4 * grp + i] = mfma32(ring[(4 * st + i) % DEPTH][j], b, out[4 * grp + i]);
+      });
+    });
+    // refill the four slots just consumed
+    static_for<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int g = 4 * st + i;
+#ifndef NERF_MLP_NOLOAD
+      if constexpr (g + DEPTH < G) ring[g % DEPTH] = wf[stream_block<NT, KSQ>(g + DEPTH) * 64];
+      else ring[g % DEPTH] = nf[(((g + DEPTH - G) % 4) * next_ksq + (g + DEPTH - G) / 4) * 64];
+#else   // timing-only build: the weight stream removed (wrong results)
+      asm volatile("" : "+v"(ring[g % DEPTH]));
+#endif
+    });
+    // keep the ring's issue order: without this the scheduler hoists the layer's weight
+    // loads and runs out of registers
     __builtin_amdgcn_sched_barrier(0);
   });
 }
 
-#endif  // NERF_MLP_OVERLAP
+// Training: store ReLU(tile) of an 8-tile activation set into the sample's save row at `off`.
+__device__ __forceinline__ void save_tiles(float* __restrict__ row, int off, const f32x16 (&t8)[8], int ntiles,
+                                           int h, bool valid) {
+  if (!valid) return;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    if (t >= ntiles) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(t8[t][4 * q + e], 0.0f);
+      *reinterpret_cast<f32x4*>(row + off + t * 32 + 8 * q + 4 * h) = v;
+    }
+  }
+}
 
+// SAVE = the training forward: also writes the per-sample activation row (layout.h kSave*) to
+// `save` (M x kSaveRow); encd (R x 32) holds each ray's PE_4(d) from nerf_ray_features.
+template <bool SAVE>
 __global__ void __launch_bounds__(64 * NERF_MLP_WAVES, 1)
 mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
            const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
-           float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
+           float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
+           float* __restrict__ save, const float* __restrict__ encd) {
   const int lane = threadIdx.x & 63;
   const int64_t s0 = ((int64_t)blockIdx.x * NERF_MLP_WAVES + (threadIdx.x >> 6)) * 32;
   if (s0 >= M) return;
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const int64_t r = s / N;
+  NERF_STAMP(0);
 
   // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
   float x[3];
@@ -300,36 +242,61 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   pe[31] = h ? 0.0f : x[2];
 #pragma unroll
   for (int p = 0; p < kPeSteps; ++p) pe_mine[p][lane] = pe[p];
+  const bool valid = s0 + (lane & 31) < M;
+  float* srow = SAVE ? save + s * kSaveRow : nullptr;
+  if constexpr (SAVE) {
+    if (valid) {
+#pragma unroll
+      for (int p = 0; p < kPeSteps; ++p) {
+        const int f = pe_feature(p, h);
+        srow[kSaveEncX + (f < 0 ? kPosEnc : f)] = f < 0 ? 0.0f : pe[p];
+      }
+      const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) reinterpret_cast<f32x4*>(srow + kSaveEncD + 16 * h)[q] = ed[q];
+    }
+  }
 
+  NERF_STAMP(1);
   const float* bias = packed + kOffBias;
   const float* wtrunk = packed + frag_offset(1);                 // layers 1..7, frag_floats(1) apart
   auto wlayer = [&](int m) { return wtrunk + (size_t)(m - 1) * frag_floats(1); };
   const float* wskip = packed + frag_offset(kSkipPeMat);
+  constexpr int Q_ACT = kActSteps / 4, Q_PE = kPeSteps / 4;
   f32x4 ring[kDepth];
-  ring_fill(ring, packed + frag_offset(0), lane);
+  ring_fill<8, Q_PE>(ring, packed + frag_offset(0), lane);
   f32x16 A[8], B[8];
-  // layer 0: PE(63) -> 256
-  dense<8, 0, kPeSteps, true, true>(packed + frag_offset(0), wlayer(1), ring, bias, A, pe, A, lane);
-  // layers 1..6 as three A->B->A pairs; the skip layer 4 adds its PE slice before its ReLU.
+  // layer 0: PE(63) -> 256 (pre-activations in A)
+  dense<8, 0, kPeSteps, kBias, false>(packed + frag_offset(0), wlayer(1), Q_ACT, ring, bias, A, pe, A, lane);
+  if constexpr (SAVE) save_tiles(srow, save_h(0), A, 8, h, valid);
+  NERF_STAMP(2);
+  // layers 1..6 as three A->B->A pairs; the skip layer 4 accumulates its PE slice onto its
+  // pre-activations (models.py:130-131).  Every layer reads ReLU(previous) as its input.
 #pragma unroll 1
   for (int p = 0; p < 3; ++p) {
     const int m1 = 1 + 2 * p, m2 = 2 + 2 * p;
-    dense<8, kActSteps, 0, true, true>(wlayer(m1), wlayer(m2), ring, bias + m1 * kHidden, A, pe, B, lane);
-    dense<8, kActSteps, 0, true, false>(wlayer(m2), m2 == kSkipLayer ? wskip : wlayer(m2 + 1), ring,
+    const bool skip = m2 == kSkipLayer;
+    dense<8, kActSteps, 0, kBias, true>(wlayer(m1), wlayer(m2), Q_ACT, ring, bias + m1 * kHidden, A, pe, B, lane);
+    if constexpr (SAVE) save_tiles(srow, save_h(m1), B, 8, h, valid);
+    NERF_STAMP(3 + 2 * p);
+    dense<8, kActSteps, 0, kBias, true>(wlayer(m2), skip ? wskip : wlayer(m2 + 1), skip ? Q_PE : Q_ACT, ring,
                                         bias + m2 * kHidden, B, pe, A, lane);
-    if (m2 == kSkipLayer) {
+    if (skip) {
       float pe2[kPeSteps];
 #pragma unroll
       for (int q = 0; q < kPeSteps; ++q) pe2[q] = pe_mine[q][lane];
-      dense<8, 0, kPeSteps, false, false>(wskip, wlayer(m2 + 1), ring, bias, A, pe2, A, lane);
+      dense<8, 0, kPeSteps, kAccum, false>(wskip, wlayer(m2 + 1), Q_ACT, ring, bias, A, pe2, A, lane);
     }
-#pragma unroll
-    for (int t = 0; t < 8; ++t) relu16(A[t]);
+    if constexpr (SAVE) save_tiles(srow, save_h(m2), A, 8, h, valid);
+    NERF_STAMP(4 + 2 * p);
   }
-  // layer 7: A -> B
-  dense<8, kActSteps, 0, true, true>(wlayer(7), packed + frag_offset(8), ring, bias + 7 * kHidden, A, pe, B, lane);
+  // layer 7: A -> B; B holds h7's pre-activations
+  dense<8, kActSteps, 0, kBias, true>(wlayer(7), packed + frag_offset(8), Q_ACT, ring, bias + 7 * kHidden, A, pe, B,
+                                      lane);
+  if constexpr (SAVE) save_tiles(srow, save_h(7), B, 8, h, valid);
+  NERF_STAMP(9);
 
-  // density head: sigma = ReLU(density_head(h)) (models.py:137-138), h = B.
+  // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138).
   const float* ws = packed + kOffSigmaW;
   float part = 0.0f;
 #pragma unroll
@@ -338,30 +305,40 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
     for (int q = 0; q < 4; ++q) {
       const f32x4 w = *reinterpret_cast<const f32x4*>(ws + t * 32 + 8 * q + 4 * h);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) part = fmaf(w[e], B[t][4 * q + e], part);
+      for (int e = 0; e < 4; ++e) part = fmaf(w[e], fmaxf(B[t][4 * q + e], 0.0f), part);
     }
   const float sig = fmaxf(part + __shfl_xor(part, 32) + packed[kOffSigmaB], 0.0f);
 
-  // colour branch: h_dir = ReLU(W_dh h + [b_dir + W_dd PE(d)]) + appearance (models.py:141-156),
-  // the bracket and the appearance part precomputed per ray in `feat`.
+  // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
+  // (models.py:141-156), the bracket and the appearance part precomputed per ray in `feat`.
   const float* fr = feat + r * kRayFeat;
-#if NERF_MLP_OVERLAP
-  dense<4, kActSteps, 0, true, true, true>(packed + frag_offset(8), packed, ring, fr, B, pe, A, lane);
-#else
-  dense<4, kActSteps, 0, true, true>(packed + frag_offset(8), packed, ring, fr, B, pe, A, lane);
-#endif
+  dense<4, kActSteps, 0, kPerLane, true>(packed + frag_offset(8), packed + frag_offset(8), Q_ACT, ring, fr, B, pe, A,
+                                         lane);
+  NERF_STAMP(10);
+  if constexpr (SAVE) save_tiles(srow, kSaveRDir, A, 4, h, valid);
   float pr[3] = {0.0f, 0.0f, 0.0f};
   const float* wr = packed + kOffRgbW;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const f32x16 app = load_rows(fr + kDirHidden, t, h);
+    if constexpr (SAVE) {
+      if (valid) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(A[t][4 * q + e], 0.0f) + app[4 * q + e];
+          *reinterpret_cast<f32x4*>(srow + kSaveHd + t * 32 + 8 * q + 4 * h) = v;
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], A[t][4 * q + e] + app[4 * q + e], pr[c]);
+        for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], fmaxf(A[t][4 * q + e], 0.0f) + app[4 * q + e], pr[c]);
       }
     }
   }
@@ -377,16 +354,22 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
   }
+  NERF_STAMP(11);
 }
 
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
-               const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s) {
+               const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
+               float* save, const float* encd) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   constexpr int per_block = 32 * NERF_MLP_WAVES;
   const int64_t blocks = (M + per_block - 1) / per_block;
-  hipLaunchKernelGGL(mlp_kernel, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M, N, feat, rgb,
-                     sigma, out_slot, out_T);
+  if (save)
+    hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M, N,
+                       feat, rgb, sigma, out_slot, out_T, save, encd);
+  else
+    hipLaunchKernelGGL(mlp_kernel<false>, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M,
+                       N, feat, rgb, sigma, out_slot, out_T, nullptr, nullptr);
   return check_launch("mlp_kernel");
 }
 
@@ -399,7 +382,8 @@ constexpr int kFeatRays = 16;
 
 __global__ void __launch_bounds__(256)
 ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ dirs, int64_t R,
-                    const float* __restrict__ app, int64_t app_rows, float* __restrict__ feat) {
+                    const float* __restrict__ app, int64_t app_rows, float* __restrict__ feat,
+                    float* __restrict__ encd) {
   __shared__ float enc[kFeatRays][kDirEnc + 1];
   __shared__ float apps[kFeatRays][kAppDim];
   const int tid = threadIdx.x;
@@ -425,6 +409,12 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
     }
   }
   __syncthreads();
+  if (encd) {   // training: each ray's PE_4(d), padded to 32
+    for (int q = tid; q < kFeatRays * 32; q += 256) {
+      const int ray = q / 32, k = q % 32;
+      if (r0 + ray < R) encd[(r0 + ray) * 32 + k] = k < kDirEnc ? enc[ray][k] : 0.0f;
+    }
+  }
   const int n = tid;
   float acc[kFeatRays];
   if (n < kDirHidden) {
@@ -457,10 +447,10 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
 }
 
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
-                        int64_t app_rows, float* feat, hipStream_t s) {
+                        int64_t app_rows, float* feat, hipStream_t s, float* encd) {
   if (R == 0) return NERF_OK;
   hipLaunchKernelGGL(ray_features_kernel, dim3((unsigned)((R + kFeatRays - 1) / kFeatRays)), dim3(256), 0, s,
-                     packed, dirs, R, app, app_rows, feat);
+                     packed, dirs, R, app, app_rows, feat, encd);
   return check_launch("ray_features_kernel");
 }
 

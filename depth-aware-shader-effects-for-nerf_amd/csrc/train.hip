@@ -1,0 +1,745 @@
+// Training path (BASELINE config 5): backward of the render path and the
+// optimizer step, all hand-written for gfx950.
+//
+// Reference: src/train.py:13-207 — volume_render (perturb=True, coarse only: render.py:83-86
+// ignores n_importance), MSE against the target rgb (:87), loss.backward(), Adam (:90-92).
+//
+//   composite_backward_kernel   d loss / d(sigma, rgb) per sample from d loss / d rgb_map (one
+//                               wave per ray, reverse double-precision scan)
+//   mlp_backward_kernel         the data-gradient chain of NeRF.forward on fp32 MFMA, one wave per
+//                               32 samples, mirroring mlp_kernel with transposed weights: writes
+//                               every layer's d loss / d pre-activation (layout.h kGrad*)
+//   wgrad_kernel + reduce       dW[n][k] = sum_m dpre[m][n] x[m][k] (+ the bias column) over the
+//                               batch, chunked over samples with a deterministic reduction
+//   app_grad_kernel             per-ray appearance-embedding gradient
+//   adam_kernel                 torch.optim.Adam's update, element for element
+#include <utility>
+
+#include "common.h"
+
+namespace nerf {
+
+static_assert(kSaveRow == NERF_SAVE_ROW && kGradRow == NERF_GRAD_ROW, "nerfmi_train.h rows out of sync");
+
+// ---------------------------------------------------------------------------- composite bwd
+// render.py:56-80 differentiated.  With g = d loss / d rgb_map (3), per sample s of a ray:
+//   drgb_s = w_s g;  dw_s = g . rgb_s;  T_s = prod_{j<s} f_j, f_j = 1 - a_j + 1e-10
+//   d a_s = dw_s T_s - (1/f_s) sum_{t>s} dw_t w_t;   d sigma_s = d a_s * dist_s * exp(-sigma_s dist_s)
+// The loss is mean((rgb_map - target)^2) over B x 3 (train.py:87): g = 2 (rgb_map - target)/(3B);
+// sq_err[r] = sum_c (rgb_map - target)^2 for the loss value.
+__global__ void __launch_bounds__(256)
+composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma, const float* __restrict__ zv,
+                          const float* __restrict__ rgb_map, const float* __restrict__ target, int64_t B, int N,
+                          float scale, float* __restrict__ dsigma, float* __restrict__ drgb,
+                          float* __restrict__ sq_err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  const int64_t base = r * N;
+  float g[3], se = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float e = rgb_map[3 * r + c] - target[3 * r + c];
+    g[c] = scale * e;
+    se += e * e;
+  }
+  if (lane == 0) sq_err[r] = se;
+  if (N == 1) {                       // the reference's per-sample tensors are empty (render.py:56-58)
+    if (lane == 0) {
+      dsigma[base] = 0.0f;
+      drgb[3 * base] = drgb[3 * base + 1] = drgb[3 * base + 2] = 0.0f;
+    }
+    return;
+  }
+  // pass 1 (forward order): transmittance prefix, carried across 64-sample chunks
+  // pass 2 (reverse order): suffix sums of dw*w; done chunk by chunk from the end, recomputing
+  // each chunk's T from the stored chunk-start prefixes.
+  const int nchunk = (N + 63) / 64;
+  __shared__ double carry_lds[4][64]; // T at each chunk start (N <= 4096)
+  double* carry_chunk = carry_lds[threadIdx.x >> 6];
+  double carry = 1.0;
+  for (int c = 0; c < nchunk; ++c) {
+    const int s = c * 64 + lane;
+    double f = 1.0;
+    if (s < N) {
+      const float z = zv[base + s];
+      const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
+      const float alpha = 1.0f - expf(-sigma[base + s] * dist);
+      f = (double)((1.0f - alpha) + 1e-10f);
+    }
+    double incl = f;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double up = __shfl_up(incl, off);
+      if (lane >= off) incl *= up;
+    }
+    if (lane == 0) carry_chunk[c] = carry;
+    carry *= __shfl(incl, 63);
+  }
+  __builtin_amdgcn_wave_barrier();
+  double suffix = 0.0;                // sum_{t > current chunk} dw_t w_t
+  for (int c = nchunk - 1; c >= 0; --c) {
+    const int s = c * 64 + lane;
+    const bool valid = s < N;
+    float alpha = 0.0f, dist = 0.0f, e = 1.0f, fs = 1.0f, sg = 0.0f;
+    double f = 1.0;
+    if (valid) {
+      const float z = zv[base + s];
+      dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
+      sg = sigma[base + s];
+      e = expf(-sg * dist);
+      alpha = 1.0f - e;
+      fs = (1.0f - alpha) + 1e-10f;
+      f = (double)fs;
+    }
+    double incl = f;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double up = __shfl_up(incl, off);
+      if (lane >= off) incl *= up;
+    }
+    double excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 1.0;
+    const float T = (float)(carry_chunk[c] * excl);
+    const float w = alpha * T;
+    float dw = 0.0f;
+    if (valid) {
+      const int64_t e3 = 3 * (base + s);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dw += g[k] * rgb[e3 + k];
+        drgb[e3 + k] = w * g[k];
+      }
+    }
+    // exclusive suffix sum of dw*w inside the chunk, plus the chunks after it
+    double v = valid ? (double)dw * (double)w : 0.0;
+    double incl_rev = v;                                   // inclusive suffix within the chunk
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double dn = __shfl_down(incl_rev, off);
+      if (lane + off < 64) incl_rev += dn;
+    }
+    const double excl_rev = incl_rev - v + suffix;
+    if (valid) {
+      const float da = (float)((double)dw * (double)T - excl_rev / (double)fs);
+      dsigma[base + s] = da * dist * e;
+    }
+    suffix += __shfl(incl_rev, 0);
+  }
+}
+
+int launch_composite_backward(const float* rgb, const float* sigma, const float* z, const float* rgb_map,
+                              const float* target, int64_t B, int N, float scale, float* dsigma, float* drgb,
+                              float* sq_err, hipStream_t s) {
+  if (B == 0) return NERF_OK;
+  hipLaunchKernelGGL(composite_backward_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, rgb, sigma, z,
+                     rgb_map, target, B, N, scale, dsigma, drgb, sq_err);
+  return check_launch("composite_backward_kernel");
+}
+
+// ------------------------------------------------------------------------ transposed weights
+// Fragment layout (layout.h) of W_l^T for trunk layers 1..7 (act part of layer 4) and of the
+// h-part of dir_linear: matrix mt = 0..6 is W_{mt+1}^T (256 x 256), mt = 7 is W_dh^T (256 x 128).
+// Rows are the forward layer's INPUT neurons (natural order), columns its OUTPUT neurons in the
+// accumulator k order, so the backward chain feeds d pre-activations to the MFMA as they sit
+// in registers, exactly like the forward.
+NERF_HD constexpr int tmat_ksteps(int mt) { return mt == 7 ? kDirHidden / 2 : kActSteps; }
+NERF_HD constexpr size_t tmat_offset(int mt) { return (size_t)mt * 8 * kActSteps * 64; }
+constexpr size_t kPackedTFloats = tmat_offset(7) + (size_t)8 * (kDirHidden / 2) * 64;   // 491520
+
+NERF_HD inline float packT_value(const float* const* P, size_t e) {
+  int mt = (int)(e / (8 * kActSteps * 64));
+  if (mt > 7) mt = 7;
+  const size_t rel = e - tmat_offset(mt);
+  const int j = (int)(rel & 3);
+  const int lane = (int)((rel >> 2) & 63);
+  const size_t blk = rel >> 8;
+  const int ksq = tmat_ksteps(mt) / 4;
+  const int nt = (int)(blk / ksq), kq = (int)(blk % ksq);
+  const int o = act_feature(4 * kq + j, lane >> 5);       // forward output neuron
+  const int i = nt * 32 + (lane & 31);                   // forward input neuron
+  if (mt == 7) return P[P_DIR_W][(size_t)o * (kHidden + kDirEnc) + i];
+  const int layer = mt + 1;
+  const int K = layer == kSkipLayer ? kHidden + kPosEnc : kHidden;
+  return P[2 * layer][(size_t)o * K + i];
+}
+
+struct ParamPtrsT { const float* p[P_COUNT]; };
+
+__global__ void __launch_bounds__(256) packT_kernel(ParamPtrsT P, float* __restrict__ packed) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < kPackedTFloats) packed[e] = packT_value(P.p, e);
+}
+
+int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
+  ParamPtrsT P;
+  for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
+  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedTFloats + 255) / 256)), dim3(256), 0, s, P, packedT);
+  return check_launch("packT_kernel");
+}
+
+void packT_host(const float* const* params, float* packedT) {
+  for (size_t e = 0; e < kPackedTFloats; ++e) packedT[e] = packT_value(params, e);
+}
+
+// ------------------------------------------------------------------------------ MLP backward
+__device__ __forceinline__ f32x16 mfma32t(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <typename F, int... Is>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// out (8 tiles, 256 forward-input neurons) = W^T . in (KS k-steps of forward-output neurons in
+// accumulator order), from a transposed fragment matrix.  Four tiles interleaved (independent
+// MFMAs); weights streamed through a DEPTH-block register ring.
+template <int KS>
+__device__ __forceinline__ void dgrad(const float* __restrict__ wmat, const f32x16 (&in)[8], f32x16 (&out)[8],
+                                      int lane) {
+  constexpr int KSQ = KS / 4;
+  constexpr int DEPTH = 8;
+  constexpr int G = 8 * KSQ;
+  const f32x4* __restrict__ wf = reinterpret_cast<const f32x4*>(wmat) + lane;
+  auto blk = [](int g) { return ((g / (4 * KSQ)) * 4 + g % 4) * KSQ + (g / 4) % KSQ; };
+  f32x4 ring[DEPTH];
+#pragma unroll
+  for (int p = 0; p < DEPTH; ++p) ring[p] = wf[blk(p) * 64];
+  sfor<G / 4>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int st = decltype(sc)::value;
+    constexpr int grp = st / KSQ, kq = st % KSQ;
+    if constexpr (kq == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[4 * grp + i] = f32x16{};
+    }
+    sfor<4>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int ks = 4 * kq + j;
+      const float b = in[ks >> 4][ks & 15];
+      sfor<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        out[4 * grp + i] = mfma32t(ring[(4 * st + i) % DEPTH][j], b, out[4 * grp + i]);
+      });
+    });
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int g = 4 * st + i;
+      if constexpr (g + DEPTH < G) ring[g % DEPTH] = wf[blk(g + DEPTH) * 64];
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+// d pre-activation = d activation * [activation > 0] (ReLU backward; the saved activation is
+// ReLU(pre), positive exactly where pre is), in place, and stored to the gradient row.
+__device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, const float* __restrict__ srow,
+                                                int save_off, float* __restrict__ grow, int grad_off, int h,
+                                                bool valid) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    if (t >= ntiles) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(srow + save_off + t * 32 + 8 * q + 4 * h);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = a[e] > 0.0f ? x[t][4 * q + e] : 0.0f;
+        x[t][4 * q + e] = d;
+        v[e] = d;
+      }
+      if (valid) *reinterpret_cast<f32x4*>(grow + grad_off + t * 32 + 8 * q + 4 * h) = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256, 1)
+mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
+                    const float* __restrict__ save, const float* __restrict__ sigma, const float* __restrict__ rgb,
+                    const float* __restrict__ dsigma, const float* __restrict__ drgb, int64_t M,
+                    float* __restrict__ grad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
+  if (s0 >= M) return;
+  const int h = lane >> 5;
+  const int64_t s = imin64(s0 + (lane & 31), M - 1);
+  const bool valid = s0 + (lane & 31) < M;
+  const float* srow = save + s * kSaveRow;
+  float* grow = grad + s * kGradRow;
+
+  // rgb head: rgb = sigmoid(v) -> dv = drgb * rgb (1 - rgb) (models.py:159-160)
+  float dv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float y = rgb[3 * s + c];
+    dv[c] = drgb[3 * s + c] * (y * (1.0f - y));
+  }
+  // density head: sigma = ReLU(v_s) -> d v_s = dsigma * [sigma > 0]
+  const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
+  if (valid && h == 0) {
+    grow[kGradSigma] = dsp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+  }
+  f32x16 A[8], B[8];
+  // d hd = W_rgb^T dv (128, accumulator layout in A[0..3])
+  const float* wr = packed + kOffRgbW;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = t * 32 + 8 * q + 4 * h + e;
+        const float d = fmaf(dv[2], wr[2 * kDirHidden + n], fmaf(dv[1], wr[kDirHidden + n], dv[0] * wr[n]));
+        A[t][4 * q + e] = d;
+        v[e] = d;
+      }
+      if (valid) *reinterpret_cast<f32x4*>(grow + kGradHd + t * 32 + 8 * q + 4 * h) = v;
+    }
+  // hd = ReLU(dir pre) + appearance: d dir_pre = d hd * [r_dir > 0]
+  relu_back_store(A, 4, srow, kSaveRDir, grow, kGradDir, h, valid);
+  // d h7 = W_dh^T d dir_pre + w_sigma * d v_s
+  dgrad<kDirHidden / 2>(packedT + tmat_offset(7), A, B, lane);
+  const float* wsg = packed + kOffSigmaW;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wsg + t * 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) B[t][4 * q + e] = fmaf(dsp, w[e], B[t][4 * q + e]);
+    }
+  // trunk, top down: d pre_l = d h_l [h_l > 0]; d h_{l-1} = W_l^T d pre_l
+#pragma unroll 1
+  for (int p = 0; p < 3; ++p) {
+    const int l1 = 7 - 2 * p, l2 = 6 - 2 * p;
+    relu_back_store(B, 8, srow, save_h(l1), grow, l1 * kHidden, h, valid);
+    dgrad<kActSteps>(packedT + tmat_offset(l1 - 1), B, A, lane);
+    relu_back_store(A, 8, srow, save_h(l2), grow, l2 * kHidden, h, valid);
+    dgrad<kActSteps>(packedT + tmat_offset(l2 - 1), A, B, lane);
+  }
+  relu_back_store(B, 8, srow, save_h(1), grow, 1 * kHidden, h, valid);
+  dgrad<kActSteps>(packedT + tmat_offset(0), B, A, lane);
+  relu_back_store(A, 8, srow, save_h(0), grow, 0, h, valid);
+}
+
+int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
+                        const float* rgb, const float* dsigma, const float* drgb, int64_t M, float* grad,
+                        hipStream_t s) {
+  if (M == 0) return NERF_OK;
+  hipLaunchKernelGGL(mlp_backward_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT, save,
+                     sigma, rgb, dsigma, drgb, M, grad);
+  return check_launch("mlp_backward_kernel");
+}
+
+// ---------------------------------------------------------------------------------- wgrad
+// partial[c][n][k'] = sum over samples m of chunk c of a[m][n] * x'[m][k'], k' < K + 1, where
+// x'[m][k] = x[xrow(m)][k] for k < K and x'[m][K] = 1 (the bias column).  xrow(m) = m / x_div
+// (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).
+// One wave computes a 32 (n) x 64 (k') tile of one chunk on v_mfma_f32_32x32x2_f32 (two samples
+// per MFMA): A = a^T fragment (lane: n = l&31, sample = l>>5), B = x' fragment (sample = l>>5,
+// k = l&31); loads are 128 contiguous bytes per half-wave.
+constexpr int kWChunk = 2048;   // samples per chunk
+
+__global__ void __launch_bounds__(256)
+wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
+             int64_t x_div, int64_t M, float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int KP = K + 1;
+  const int ntn = (N + 31) / 32, ntk = (KP + 63) / 64;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= ntn * ntk) return;
+  const int n0 = (tile / ntk) * 32, k0 = (tile % ntk) * 64;
+  const int64_t m0 = (int64_t)blockIdx.y * kWChunk;
+  const int64_t m1 = m0 + kWChunk < M ? m0 + kWChunk : M;
+  const int n = n0 + (lane & 31);
+  const int ka = k0 + (lane & 31), kb = ka + 32;
+  const int hm = lane >> 5;
+  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+  // uniform trip count for the whole wave (MFMA is a wave-wide instruction); a sample past the
+  // chunk end contributes a zero a-operand
+  const int pairs = (int)((m1 - m0 + 1) / 2);
+  const int mlast = (int)m1 - 1;
+  for (int p = 0; p < pairs; ++p) {
+    const int m = (int)m0 + 2 * p + hm;
+    const int mc = m < mlast ? m : mlast;
+    const float av = (n < N && m <= mlast) ? a[(int64_t)mc * lda + n] : 0.0f;
+    const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? mc : mc / (int)x_div);
+    const float x0 = ka < K ? x[xr * ldx + ka] : (ka == K ? 1.0f : 0.0f);
+    const float x1 = kb < K ? x[xr * ldx + kb] : (kb == K ? 1.0f : 0.0f);
+    acc0 = mfma32t(av, x0, acc0);
+    acc1 = mfma32t(av, x1, acc1);
+  }
+  float* out = partial + (size_t)blockIdx.y * N * KP;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int row = n0 + (g & 3) + 8 * (g >> 2) + 4 * hm;
+    if (row < N) {
+      if (ka < KP) out[(size_t)row * KP + ka] = acc0[g];
+      if (kb < KP) out[(size_t)row * KP + kb] = acc1[g];
+    }
+  }
+}
+
+// out_w[n][k] (ld K) and out_b[n] (nullable) += / = sum over chunks
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w,
+                    float* __restrict__ out_b, int accumulate) {
+  const int KP = K + 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * KP) return;
+  double acc = 0.0;
+  for (int c = 0; c < chunks; ++c) acc += (double)partial[(size_t)c * N * KP + idx];
+  const int n = (int)(idx / KP), k = (int)(idx % KP);
+  float* dst = k < K ? out_w + (size_t)n * K + k : (out_b ? out_b + n : nullptr);
+  if (!dst) return;
+  *dst = accumulate ? *dst + (float)acc : (float)acc;
+}
+
+size_t wgrad_workspace_floats(int64_t M, int N, int K) {
+  const int64_t chunks = (M + kWChunk - 1) / kWChunk;
+  return (size_t)chunks * N * (K + 1);
+}
+
+int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
+                 float* out_w, float* out_b, int accumulate, float* ws, hipStream_t s) {
+  if (M == 0) return NERF_OK;
+  const int KP = K + 1;
+  const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
+  const int chunks = (int)((M + kWChunk - 1) / kWChunk);
+  hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N, x,
+                     ldx, K, x_div, M, ws);
+  int rc = check_launch("wgrad_kernel");
+  if (rc) return rc;
+  const int64_t total = (int64_t)N * KP;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, chunks, N, K,
+                     out_w, out_b, accumulate);
+  return check_launch("wgrad_reduce_kernel");
+}
+
+// ------------------------------------------------------------------- appearance gradient
+// d app_row(r) = appearance_projection.weight^T . S_r, S_r = sum over the samples that used row r of
+// d hd (models.py:154-156: hd += W_app app + b_app).  Row r's samples are src rows
+// [r*group, (r+1)*group) with stride ld: per-ray rows pass the gradient rows (group = N); a single
+// broadcast row passes the already-reduced bias gradient of appearance_projection (group = 1).
+__global__ void __launch_bounds__(128)
+app_grad_kernel(const float* __restrict__ src, int64_t ld, int group, const float* __restrict__ packed,
+                float* __restrict__ dapp) {
+  __shared__ float sum[kDirHidden];
+  const int64_t r = blockIdx.x;
+  const int n = threadIdx.x;
+  double acc = 0.0;
+  for (int s = 0; s < group; ++s) acc += (double)src[(r * group + s) * ld + n];
+  sum[n] = (float)acc;
+  __syncthreads();
+  if (n < kAppDim) {
+    const float* W = packed + kOffAppW;      // (128 x 32) row-major
+    float v = 0.0f;
+    for (int j = 0; j < kDirHidden; ++j) v = fmaf(W[j * kAppDim + n], sum[j], v);
+    dapp[r * kAppDim + n] = v;
+  }
+}
+
+int launch_app_grad(const float* src, int64_t ld, int64_t rows, int group, const float* packed, float* dapp,
+                    hipStream_t s) {
+  if (rows == 0) return NERF_OK;
+  hipLaunchKernelGGL(app_grad_kernel, dim3((unsigned)rows), dim3(128), 0, s, src, ld, group, packed, dapp);
+  return check_launch("app_grad_kernel");
+}
+
+// ------------------------------------------------------------------------------------ Adam
+// torch.optim.Adam (amsgrad=False, maximize=False, weight_decay=0) element for element:
+//   m = lerp(m, g, 1-beta1);  v = v*beta2 + (1-beta2) g^2
+//   p = p - step_size * m / (sqrt(v)/bc2_sqrt + eps),  step_size = lr / bc1
+__global__ void __launch_bounds__(256)
+adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+            int64_t n, float w1, float beta2, float one_m_beta2, float bc2_sqrt, float eps, float neg_step) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  const float mi = m[i];
+  // lerp as ATen's vectorised CPU kernel evaluates it (fused multiply-add), addcmul left to right
+  const float m_new = w1 < 0.5f ? fmaf(w1, gi - mi, mi) : fmaf(w1 - 1.0f, gi - mi, gi);
+  const float v_new = v[i] * beta2 + (one_m_beta2 * gi) * gi;
+  m[i] = m_new;
+  v[i] = v_new;
+  const float denom = sqrtf(v_new) / bc2_sqrt + eps;
+  p[i] = p[i] + neg_step * (m_new / denom);
+}
+
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                double eps, int64_t step, hipStream_t s) {
+  if (n == 0) return NERF_OK;
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, g, m, v, n,
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps,
+                     (float)(-(lr / bc1)));
+  return check_launch("adam_kernel");
+}
+
+}  // namespace nerf
+
+namespace nerf {
+// loss = sum(sq_err) / (3B) (F.mse_loss, reduction='mean', train.py:87), summed in double
+__global__ void __launch_bounds__(256) loss_kernel(const float* __restrict__ sq_err, int64_t B, float* __restrict__ loss) {
+  __shared__ double part[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < B; i += 256) acc += (double)sq_err[i];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = (float)(part[0] / (3.0 * (double)B));
+}
+
+// Training workspace carve (each region 256-B aligned), M = B*N samples:
+//   dirs (B,3) | z (B,N) | feat (B,256) | encd (B,32) | rgb (M,3) | sigma (M) | maps (B,4)
+//   | dsigma (M) | drgb (M,3) | sq_err (B) | save (M,kSaveRow) | grad (M,kGradRow) | wgrad partials
+enum { T_DIRS, T_Z, T_FEAT, T_ENCD, T_RGB, T_SIG, T_MAPS, T_DSIG, T_DRGB, T_SQE, T_SAVE, T_GRAD, T_WG, T_COUNT };
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// the largest wgrad partial buffer over the parameter list of param_grads
+static size_t max_wgrad_floats(int64_t M) {
+  const int Ks[] = {kPosEnc, kHidden, kHidden + kPosEnc, kHidden + kDirEnc, kAppDim, kDirHidden};
+  size_t m = 0;
+  for (int K : Ks) {
+    const size_t f = wgrad_workspace_floats(M, kHidden, K);
+    if (f > m) m = f;
+  }
+  return m;
+}
+
+static size_t train_carve(int64_t B, int N, size_t* off) {
+  const size_t b = (size_t)B, M = b * (size_t)N;
+  const size_t sizes[T_COUNT] = {b * 3, b * N, b * kRayFeat, b * 32, M * 3, M, b * 4, M, M * 3, b,
+                                 M * kSaveRow, M * kGradRow, max_wgrad_floats((int64_t)M)};
+  size_t at = 0;
+  for (int i = 0; i < T_COUNT; ++i) {
+    off[i] = at;
+    at += align256(sizes[i] * 4);
+  }
+  return at;
+}
+}  // namespace nerf
+
+using namespace nerf;
+
+#define TREQUIRE(cond, ...)                                        \
+  do {                                                             \
+    if (!(cond)) return set_error(NERF_ERR_BAD_ARG, __VA_ARGS__);  \
+  } while (0)
+
+extern "C" {
+
+size_t nerf_packed_transposed_floats(void) { return kPackedTFloats; }
+
+int nerf_pack_weights_transposed(const float* const* params, float* packedT, nerf_stream_t stream) {
+  TREQUIRE(params && packedT, "nerf_pack_weights_transposed: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) TREQUIRE(params[i], "nerf_pack_weights_transposed: parameter %d is null", i);
+  return launch_packT(params, packedT, (hipStream_t)stream);
+}
+
+int nerf_pack_weights_transposed_host(const float* const* params, float* packedT) {
+  TREQUIRE(params && packedT, "nerf_pack_weights_transposed_host: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) TREQUIRE(params[i], "nerf_pack_weights_transposed_host: parameter %d is null", i);
+  packT_host(params, packedT);
+  return NERF_OK;
+}
+
+int nerf_ray_features_train(const float* packed, const float* dirs, int64_t R, const float* app, int64_t app_rows,
+                            float* feat, float* enc_d, nerf_stream_t stream) {
+  TREQUIRE(R >= 0, "nerf_ray_features_train: R=%lld", (long long)R);
+  TREQUIRE(app_rows == 0 || app_rows == 1 || app_rows == R, "nerf_ray_features_train: app_rows=%lld with R=%lld",
+           (long long)app_rows, (long long)R);
+  TREQUIRE(R == 0 || (packed && dirs && feat && enc_d && (app_rows == 0 || app)),
+           "nerf_ray_features_train: null pointer");
+  return launch_ray_features(packed, dirs, R, app, app_rows, feat, (hipStream_t)stream, enc_d);
+}
+
+int nerf_mlp_forward_train(const float* packed, const float* origins, const float* dirs, const float* z_vals,
+                           int64_t R, int N, const float* ray_feat, const float* enc_d, float* rgb, float* sigma,
+                           float* save, nerf_stream_t stream) {
+  TREQUIRE(R >= 0 && N >= 1, "nerf_mlp_forward_train: R=%lld N=%d", (long long)R, N);
+  TREQUIRE(R == 0 || (packed && origins && dirs && z_vals && ray_feat && enc_d && rgb && sigma && save),
+           "nerf_mlp_forward_train: null pointer");
+  return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, nullptr, 0, (hipStream_t)stream, save,
+                    enc_d);
+}
+
+int nerf_composite_backward(const float* rgb, const float* sigma, const float* z_vals, const float* rgb_map,
+                            const float* target, int64_t B, int N, float scale, float* dsigma, float* drgb,
+                            float* sq_err, nerf_stream_t stream) {
+  TREQUIRE(B >= 0, "nerf_composite_backward: B=%lld", (long long)B);
+  if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_composite_backward: N=%d (1..4096)", N);
+  TREQUIRE(B == 0 || (rgb && sigma && z_vals && rgb_map && target && dsigma && drgb && sq_err),
+           "nerf_composite_backward: null pointer");
+  return launch_composite_backward(rgb, sigma, z_vals, rgb_map, target, B, N, scale, dsigma, drgb, sq_err,
+                                   (hipStream_t)stream);
+}
+
+int nerf_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
+                      const float* rgb, const float* dsigma, const float* drgb, int64_t M, float* grad,
+                      nerf_stream_t stream) {
+  TREQUIRE(M >= 0, "nerf_mlp_backward: M=%lld", (long long)M);
+  TREQUIRE(M == 0 || (packed && packedT && save && sigma && rgb && dsigma && drgb && grad),
+           "nerf_mlp_backward: null pointer");
+  return launch_mlp_backward(packed, packedT, save, sigma, rgb, dsigma, drgb, M, grad, (hipStream_t)stream);
+}
+
+size_t nerf_wgrad_workspace_bytes(int64_t M, int N, int K) {
+  if (M < 0 || N < 1 || K < 0) return 0;
+  return wgrad_workspace_floats(M, N, K) * 4;
+}
+
+int nerf_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
+               float* out_w, float* out_b, int accumulate, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
+  TREQUIRE(M >= 0 && M < ((int64_t)1 << 31) && N >= 1 && K >= 0 && x_div >= 0, "nerf_wgrad: M=%lld N=%d K=%d",
+           (long long)M, N, K);
+  TREQUIRE(lda >= N && (K == 0 || ldx >= K), "nerf_wgrad: lda=%lld ldx=%lld", (long long)lda, (long long)ldx);
+  TREQUIRE(M == 0 || (a && (K == 0 || x) && (K == 0 || out_w) && workspace), "nerf_wgrad: null pointer");
+  if (ws_bytes < wgrad_workspace_floats(M, N, K) * 4)
+    return set_error(NERF_ERR_WORKSPACE, "nerf_wgrad: workspace %zu < %zu bytes", ws_bytes,
+                     wgrad_workspace_floats(M, N, K) * 4);
+  return launch_wgrad(a, lda, N, x, ldx, K, x_div, M, out_w, out_b, accumulate, (float*)workspace,
+                      (hipStream_t)stream);
+}
+
+// Every parameter gradient of NeRF (+ the appearance rows) from the saved activations and the
+// per-sample gradient rows; param_grads follows nerf_pack_weights' 24-pointer order.
+static int param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
+                       const float* packed, float* const* g, float* dapp, float* ws, size_t ws_floats,
+                       hipStream_t s) {
+  struct Job { const float* a; int n; const float* x; int64_t ldx; int K; int64_t xdiv; int p; };
+  const Job jobs[] = {
+      {grad + 0, kHidden, save + kSaveEncX, kSaveRow, kPosEnc, 1, 0},
+      {grad + 1 * kHidden, kHidden, save + save_h(0), kSaveRow, kHidden, 1, 2},
+      {grad + 2 * kHidden, kHidden, save + save_h(1), kSaveRow, kHidden, 1, 4},
+      {grad + 3 * kHidden, kHidden, save + save_h(2), kSaveRow, kHidden, 1, 6},
+      {grad + 4 * kHidden, kHidden, save + save_h(3), kSaveRow, kHidden + kPosEnc, 1, 8},   // [h3 | enc_x]
+      {grad + 5 * kHidden, kHidden, save + save_h(4), kSaveRow, kHidden, 1, 10},
+      {grad + 6 * kHidden, kHidden, save + save_h(5), kSaveRow, kHidden, 1, 12},
+      {grad + 7 * kHidden, kHidden, save + save_h(6), kSaveRow, kHidden, 1, 14},
+      {grad + kGradSigma, 1, save + save_h(7), kSaveRow, kHidden, 1, P_SIGMA_W},
+      {grad + kGradDir, kDirHidden, save + save_h(7), kSaveRow, kHidden + kDirEnc, 1, P_DIR_W},  // [h7 | enc_d]
+      {grad + kGradRgb, 3, save + kSaveHd, kSaveRow, kDirHidden, 1, P_RGB_W},
+  };
+  int rc;
+  for (const Job& j : jobs) {
+    if (wgrad_workspace_floats(M, j.n, j.K) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+    if ((rc = launch_wgrad(j.a, kGradRow, j.n, j.x, j.ldx, j.K, j.xdiv, M, g[j.p], g[j.p + 1], 0, ws, s))) return rc;
+  }
+  if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
+    return NERF_OK;
+  }
+  // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1)
+  const int64_t xdiv = app_rows == 1 ? 0 : N;
+  if ((rc = launch_wgrad(grad + kGradHd, kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
+                         g[P_APP_B], 0, ws, s)))
+    return rc;
+  if (!dapp) return NERF_OK;
+  if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s);
+  return launch_app_grad(grad + kGradHd, kGradRow, app_rows, N, packed, dapp, s);
+}
+
+int nerf_param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
+                     const float* packed, float* const* param_grads_out, float* dapp, void* workspace,
+                     size_t ws_bytes, nerf_stream_t stream) {
+  TREQUIRE(M >= 0 && M < ((int64_t)1 << 31) && N >= 1 && M % N == 0, "nerf_param_grads: M=%lld N=%d",
+           (long long)M, N);
+  TREQUIRE(app_rows == 0 || app_rows == 1 || app_rows * N == M, "nerf_param_grads: app_rows=%lld", (long long)app_rows);
+  TREQUIRE(param_grads_out && packed && workspace && (M == 0 || (save && grad)) && (app_rows == 0 || app),
+           "nerf_param_grads: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) TREQUIRE(param_grads_out[i], "nerf_param_grads: gradient %d is null", i);
+  if (M == 0) return NERF_OK;
+  return param_grads(save, grad, M, N, app, app_rows, packed, param_grads_out, dapp, (float*)workspace, ws_bytes / 4,
+                     (hipStream_t)stream);
+}
+
+size_t nerf_param_grads_workspace_bytes(int64_t M) { return M < 0 ? 0 : max_wgrad_floats(M) * 4; }
+
+int nerf_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr, double beta1,
+              double beta2, double eps, int64_t step, nerf_stream_t stream) {
+  TREQUIRE(n >= 0 && step >= 1, "nerf_adam: n=%lld step=%lld", (long long)n, (long long)step);
+  TREQUIRE(n == 0 || (param && grad && exp_avg && exp_avg_sq), "nerf_adam: null pointer");
+  return launch_adam(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, (hipStream_t)stream);
+}
+
+size_t nerf_train_workspace_bytes(int64_t B, int N) {
+  if (B < 0 || N < 1) return 0;
+  size_t off[T_COUNT];
+  return train_carve(B, N, off);
+}
+
+int nerf_train_forward(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
+                       double far, int N, const float* t_vals, int perturb, const float* t_rand, uint64_t seed,
+                       const float* app, int64_t app_rows, float* rgb_map, float* depth_map, void* workspace,
+                       size_t ws_bytes, nerf_stream_t stream) {
+  TREQUIRE(B >= 0, "nerf_train_forward: B=%lld", (long long)B);
+  if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_train_forward: N=%d (1..4096)", N);
+  TREQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_train_forward: app_rows=%lld with B=%lld",
+           (long long)app_rows, (long long)B);
+  if (B == 0) return NERF_OK;
+  TREQUIRE((int64_t)B * N < ((int64_t)1 << 31), "nerf_train_forward: B*N=%lld too large", (long long)B * N);
+  TREQUIRE(packed && rays_o && rays_d && t_vals && rgb_map && depth_map && workspace && (app_rows == 0 || app),
+           "nerf_train_forward: null pointer");
+  size_t off[T_COUNT];
+  const size_t need = train_carve(B, N, off);
+  if (ws_bytes < need) return set_error(NERF_ERR_WORKSPACE, "nerf_train_forward: workspace %zu < %zu bytes", ws_bytes, need);
+  char* ws = (char*)workspace;
+  auto R = [&](int i) { return (float*)(ws + off[i]); };
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = launch_normalize(rays_d, B, R(T_DIRS), s))) return rc;                                    // render.py:19
+  if ((rc = launch_stratified(rays_o, R(T_DIRS), B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand,
+                              seed, R(T_Z), nullptr, s)))
+    return rc;                                                                                          // :22
+  if ((rc = launch_ray_features(packed, R(T_DIRS), B, app, app_rows, R(T_FEAT), s, R(T_ENCD)))) return rc;
+  if ((rc = launch_mlp(packed, rays_o, R(T_DIRS), R(T_Z), B, N, R(T_FEAT), R(T_RGB), R(T_SIG), nullptr, 0, s,
+                       R(T_SAVE), R(T_ENCD))))
+    return rc;                                                                                          // :49
+  return launch_composite(R(T_RGB), R(T_SIG), R(T_Z), B, N, rgb_map, depth_map, nullptr, s);           // :56-80
+}
+
+int nerf_train_backward(const float* packed, const float* packedT, const float* rgb_map, const float* target,
+                        int64_t B, int N, const float* app, int64_t app_rows, float* const* param_grads_out,
+                        float* dapp, float* loss, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
+  TREQUIRE(B >= 0 && N >= 1 && N <= 4096, "nerf_train_backward: B=%lld N=%d", (long long)B, N);
+  TREQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_train_backward: app_rows=%lld", (long long)app_rows);
+  TREQUIRE(packed && packedT && param_grads_out && loss && workspace && (B == 0 || (rgb_map && target)) &&
+               (app_rows == 0 || app),
+           "nerf_train_backward: null pointer");
+  for (int i = 0; i < P_COUNT; ++i) TREQUIRE(param_grads_out[i], "nerf_train_backward: gradient %d is null", i);
+  if (B == 0) return NERF_OK;
+  size_t off[T_COUNT];
+  const size_t need = train_carve(B, N, off);
+  if (ws_bytes < need) return set_error(NERF_ERR_WORKSPACE, "nerf_train_backward: workspace %zu < %zu bytes", ws_bytes, need);
+  char* ws = (char*)workspace;
+  auto R = [&](int i) { return (float*)(ws + off[i]); };
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t M = B * N;
+  int rc;
+  const float scale = (float)(2.0 / (3.0 * (double)B));                                              // train.py:87
+  if ((rc = launch_composite_backward(R(T_RGB), R(T_SIG), R(T_Z), rgb_map, target, B, N, scale, R(T_DSIG),
+                                      R(T_DRGB), R(T_SQE), s)))
+    return rc;
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, R(T_SQE), B, loss);
+  if ((rc = check_launch("loss_kernel"))) return rc;
+  if ((rc = launch_mlp_backward(packed, packedT, R(T_SAVE), R(T_SIG), R(T_RGB), R(T_DSIG), R(T_DRGB), M, R(T_GRAD), s)))
+    return rc;
+  const size_t wg_floats = (need - off[T_WG]) / 4;
+  return param_grads(R(T_SAVE), R(T_GRAD), M, N, app, app_rows, packed, param_grads_out, dapp, R(T_WG), wg_floats, s);
+}
+
+}  // extern "C"

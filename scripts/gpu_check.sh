@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU-box validation: each step under its own time limit; stops at the first crash/abort/timeout
+# (status >= 124), continues past ordinary test failures.  Usage: scripts/gpu_check.sh step...
+#   steps: variants | pytest | pytest_train | bench | smoke
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    variants) run variants 300 python scripts/mlp_variants.py ;;
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytest_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    pytest_train) run pytest_train 600 python -m pytest tests/test_gpu_train.py -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -15,6 +15,8 @@ libs = {"tree": _lib.load()}
 for p in sorted(glob.glob(os.path.join(PKG, "build", "variants", "libnerfmi_*.so"))):
     L = ctypes.CDLL(p)
     for name, (res, args) in _lib._SIGNATURES.items():
+        if not hasattr(L, name):
+            continue
         f = getattr(L, name); f.restype = res; f.argtypes = args
     libs[os.path.basename(p)[10:-3]] = L
 torch.manual_seed(0)

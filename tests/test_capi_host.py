@@ -13,11 +13,11 @@ from conftest import REPO
 from oracle import nerf_oracle as O
 from nerfmi import _lib
 
-HEADER = os.path.join(REPO, "include", "nerfmi.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("nerfmi.h", "nerfmi_train.h")]
 
 
 def header_symbols():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"\b(nerf_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -27,8 +27,8 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 14
     for s in syms:
         assert hasattr(lib, s), s
-    assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/nerfmi.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 2
+    assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -45,6 +45,16 @@ def test_bad_arguments_are_reported_not_launched():
     assert lib.nerf_render_workspace_bytes(-1, 64, 0) == 0
     # empty inputs are a no-op, not an error
     assert lib.nerf_composite(None, None, None, 0, 64, None, None, None, None) == 0
+    # training entry points
+    rc = lib.nerf_composite_backward(None, None, None, None, None, 4, 64, 1.0, None, None, None, None)
+    assert rc == 1 and b"null pointer" in lib.nerf_last_error()
+    assert lib.nerf_composite_backward(None, None, None, None, None, 4, 5000, 1.0, None, None, None, None) == 3
+    assert lib.nerf_adam(None, None, None, None, 8, 1e-3, .9, .999, 1e-8, 0, None) == 1   # step counts from 1
+    assert lib.nerf_wgrad(None, 1, 4, None, 4, 4, 1, 8, None, None, 0, None, 0, None) == 1
+    ws = lib.nerf_wgrad_workspace_bytes(5000, 256, 256)
+    assert ws == 3 * 256 * 257 * 4                      # 2048-sample chunks x N x (K + bias column)
+    assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2308) * 4
+    assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, 0, None, None) == 0
 
 
 def host_pack(state):
@@ -160,3 +170,102 @@ def test_emulated_kernel_matches_oracle(ref_state, app_vec):
         rgb_o, sigma_o = O.nerf_forward(ref_state, x, d, app)
         np.testing.assert_allclose(rgb, rgb_o.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(sigma, sigma_o.numpy(), rtol=1e-4, atol=1e-6)
+
+
+def host_pack_transposed(state):
+    lib = _lib.load()
+    ts = [state[k].contiguous().float() for k in O.STATE_KEYS]
+    arr = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+    out = np.empty(lib.nerf_packed_transposed_floats(), dtype=np.float32)
+    assert lib.nerf_pack_weights_transposed_host(arr, out.ctypes.data) == 0
+    return out
+
+
+def tfrag_matrix(packedT, mt):
+    """Transposed fragment matrix mt as the backward kernel sees it: [i][slot], slot = 2*ks + h."""
+    ks = 64 if mt == 7 else 128
+    off = mt * 8 * 128 * 64
+    blk = packedT[off: off + 8 * ks * 64].reshape(8, ks // 4, 2, 32, 4)
+    return blk.transpose(0, 3, 1, 4, 2).reshape(256, ks * 2).astype(np.float64)
+
+
+def test_transposed_fragments_are_permuted_weight_transposes(ref_state):
+    packedT = host_pack_transposed(ref_state)
+    assert packedT.size == 7 * 256 * 256 + 256 * 128
+    for layer in range(1, 8):
+        W = ref_state[f"pts_linears.{layer}.weight"].numpy()[:, :256]        # [out][in]
+        cols = [act_feature(s // 2, s % 2) for s in range(256)]
+        assert np.array_equal(tfrag_matrix(packedT, layer - 1), W.T[:, cols]), layer
+    Wd = ref_state["dir_linear.weight"].numpy()[:, :256]                     # (128, 256)
+    cols = [act_feature(s // 2, s % 2) for s in range(128)]
+    assert np.array_equal(tfrag_matrix(packedT, 7), Wd.T[:, cols])
+
+
+def emulate_backward(packed, packedT, x, d, app, g_rgb, g_sigma):
+    """The backward kernel's dataflow (csrc/train.hip mlp_backward_kernel) in float64: the
+    transposed fragments applied to d pre-activations in accumulator order, returning the
+    gradient with respect to the PE input and to every trunk pre-activation."""
+    off_bias = frag_offset(10)
+    off_sw = off_bias + 8 * 256
+    off_sb = off_sw + 256
+    off_db = off_sb + 4
+    off_dwd = off_db + 128
+    off_aw = off_dwd + 128 * 27
+    off_ab = off_aw + 128 * 32
+    off_rw = off_ab + 128
+    off_rb = off_rw + 3 * 128
+    p = packed.astype(np.float64)
+    enc = O.positional_encoding(torch.from_numpy(x), 10).numpy().astype(np.float64)
+    pe_slots = np.stack([enc[:, pe_feature(s // 2, s % 2)] if pe_feature(s // 2, s % 2) >= 0
+                         else np.zeros(len(x)) for s in range(64)], 1)
+    act = [act_feature(s // 2, s % 2) for s in range(256)]
+    bias = p[off_bias: off_bias + 8 * 256].reshape(8, 256)
+    hs = [np.maximum(pe_slots @ frag_matrix(packed, 0).T + bias[0], 0)]
+    for m in range(1, 8):
+        pre = hs[-1][:, act] @ frag_matrix(packed, m).T + bias[m]
+        if m == 4:
+            pre += pe_slots @ frag_matrix(packed, 9).T
+        hs.append(np.maximum(pre, 0))
+    h7 = hs[-1]
+    sig = np.maximum(h7 @ p[off_sw: off_sw + 256] + p[off_sb], 0)
+    encd = O.positional_encoding(torch.from_numpy(d), 4).numpy().astype(np.float64)
+    dvec = p[off_db: off_db + 128] + encd @ p[off_dwd: off_dwd + 128 * 27].reshape(128, 27).T
+    appf = np.zeros(128) if app is None else p[off_ab: off_ab + 128] + app.astype(np.float64) @ \
+        p[off_aw: off_aw + 128 * 32].reshape(128, 32).T
+    rdir = np.maximum(h7[:, act] @ frag_matrix(packed, 8).T + dvec, 0)
+    hd = rdir + appf
+    Wr = p[off_rw: off_rw + 384].reshape(3, 128)
+    rgb = 1 / (1 + np.exp(-(hd @ Wr.T + p[off_rb: off_rb + 3])))
+    # backward, mirroring the kernel
+    dv = g_rgb * rgb * (1 - rgb)
+    dhd = dv @ Wr
+    dpre_dir = dhd * (rdir > 0)
+    dh = dpre_dir[:, act[:128]] @ tfrag_matrix(packedT, 7).T
+    dh += np.where(sig > 0, g_sigma, 0)[:, None] * p[off_sw: off_sw + 256]
+    dpre = {}
+    for layer in range(7, -1, -1):
+        dpre[layer] = dh * (hs[layer] > 0)
+        if layer:
+            dh = dpre[layer][:, act] @ tfrag_matrix(packedT, layer - 1).T
+    return dpre, dpre_dir, dhd
+
+
+def test_emulated_backward_matches_autograd(ref_state, app_vec):
+    """The transposed-fragment chain reproduces torch autograd on the oracle's forward."""
+    packed, packedT = host_pack(ref_state), host_pack_transposed(ref_state)
+    torch.manual_seed(6)
+    x = torch.randn(128, 3, dtype=torch.float64) * 1.5
+    d = torch.nn.functional.normalize(torch.randn(128, 3, dtype=torch.float64), dim=-1)
+    g_rgb = torch.randn(128, 3, dtype=torch.float64)
+    g_sigma = torch.randn(128, dtype=torch.float64)
+    state = {k: v.double().requires_grad_(True) for k, v in ref_state.items()}
+    pres = []
+    rgb, sigma = O.nerf_forward(state, x, d, app_vec.double(), keep=pres)
+    for t in pres:
+        t.retain_grad()
+    (rgb * g_rgb).sum().backward(retain_graph=True)
+    (sigma[:, 0] * g_sigma).sum().backward()
+    dpre, _, _ = emulate_backward(packed, packedT, x.numpy(), d.numpy(), app_vec.numpy(), g_rgb.numpy(),
+                                  g_sigma.numpy())
+    for layer in range(8):
+        np.testing.assert_allclose(dpre[layer], pres[layer].grad.numpy(), rtol=1e-4, atol=1e-7)

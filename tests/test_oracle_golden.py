@@ -142,3 +142,32 @@ def test_fine_pass_conditioning(golden, ref_state, app_vec):
     rel = ((a - b).abs() / a.abs()).max()
     assert float(rel) > 1e-6          # a single ulp of weight noise is visible end to end
     assert float(rel) < 1e-3
+
+
+def test_oracle_train_step_matches_reference_f7(golden, golden_meta, ref_state):
+    """F7: the oracle's training step (autograd over the restatement + torch Adam) reproduces the
+    reference's loss, gradients and updated parameters (train.py:77-92)."""
+    f7 = golden("f7_train_step.npz")
+    meta = golden_meta["F7"]
+    state = {k: v.clone() for k, v in ref_state.items()}
+    torch.manual_seed(1)
+    app_table = torch.randn(100, 32)
+    t_rand = seeded_uniform(meta["seed_t_rand"], (256, 64), meta["t_rand_sha256"])
+    loss, rgb, grads, _ = O.train_step(state, app_table, 0, torch.from_numpy(f7["o"]), torch.from_numpy(f7["d"]),
+                                       torch.from_numpy(f7["target"]), 2.0, 6.0, 64, t_rand, lr=meta["lr"])
+    np.testing.assert_allclose(rgb.numpy(), f7["rgb"], rtol=1e-5, atol=1e-6)
+    assert abs(float(loss) - meta["loss"]) <= 1e-6 * meta["loss"]
+    params = dict(state, appearance_embeddings=app_table)
+    for name in meta["names"]:
+        g = grads[name]
+        assert abs(float(g.double().norm()) - meta["grad_l2"][name]) <= 1e-4 * meta["grad_l2"][name] + 1e-12, name
+        if f"idx/{name}" in f7:
+            idx = torch.from_numpy(f7[f"idx/{name}"])
+            np.testing.assert_allclose(g.reshape(-1)[idx].numpy(), f7[f"grad/{name}"], rtol=1e-3, atol=1e-9,
+                                       err_msg=name)
+            np.testing.assert_allclose(params[name].detach().reshape(-1)[idx].numpy(), f7[f"param/{name}"],
+                                       rtol=1e-6, atol=1e-7, err_msg=name)
+        else:
+            np.testing.assert_allclose(g.numpy(), f7[f"grad/{name}"], rtol=1e-3, atol=1e-9, err_msg=name)
+            np.testing.assert_allclose(params[name].detach().numpy(), f7[f"param/{name}"], rtol=1e-6, atol=1e-7,
+                                       err_msg=name)
