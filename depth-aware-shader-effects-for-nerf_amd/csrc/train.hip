@@ -389,6 +389,127 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
   }
 }
 
+// The main weight-gradient kernel: a 128 (n) x 128 (k) output tile of one 2048-sample chunk per
+// workgroup, samples streamed through LDS 16 at a time (double-buffered: the next stage's global
+// loads are in flight while the current stage's MFMAs run).  Four waves in a 2 x 2 arrangement,
+// each owning 64 x 64 = 2 x 2 accumulator tiles of v_mfma_f32_32x32x2_f32; per k-step (two
+// samples) a wave reads 4 operand values from LDS for 4 MFMAs.  The bias column (sum over
+// samples of a[m][n]) is accumulated from the staged a values by the k-tile-0 workgroups on the
+// VALU.  Blocks that share a chunk are launched 8 apart, so they land on the same XCD and the
+// chunk's rows are fetched from HBM once per L2 (blockIdx -> XCD is round-robin).
+// Preconditions (host-checked): a, x 16-byte aligned, lda % 4 == 0, ldx % 4 == 0.
+constexpr int kWT = 128;       // output tile edge
+constexpr int kWS = 16;        // samples per LDS stage
+constexpr int kWPad = 160;     // LDS row stride in floats (row s+1 lands 32 banks away)
+
+__device__ __forceinline__ f32x4 load4_masked(const float* __restrict__ p, int valid) {
+  if (valid >= 4) return *reinterpret_cast<const f32x4*>(p);
+  f32x4 v;
+  v[0] = valid > 0 ? p[0] : 0.0f;
+  v[1] = valid > 1 ? p[1] : 0.0f;
+  v[2] = valid > 2 ? p[2] : 0.0f;
+  v[3] = 0.0f;
+  return v;
+}
+
+__global__ void __launch_bounds__(256, 2)
+wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
+                 int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
+  __shared__ float As[2][kWS][kWPad];
+  __shared__ float Xs[2][kWS][kWPad];
+  __shared__ float bsum[8][kWT];
+  const int b = blockIdx.x;
+  const int grp = b / (8 * tiles), rem = b % (8 * tiles);
+  const int chunk = grp * 8 + (rem & 7);
+  const int tile = rem >> 3;
+  if (chunk >= chunks) return;                     // uniform over the block, before any barrier
+  const int n0 = (tile / ntk) * kWT, k0 = (tile % ntk) * kWT;
+  const bool do_bias = (tile % ntk) == 0;
+  const int64_t m0 = (int64_t)chunk * kWChunk;
+  const int64_t m1 = m0 + kWChunk < M ? m0 + kWChunk : M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wn = w & 1, wk = w >> 1;
+  const int lr = tid >> 5, lc = (tid & 31) * 4;
+  const int an = n0 + lc, xk = k0 + lc;
+  const int a_valid = N - an, x_valid = K - xk;
+  f32x4 ra0, ra1, rx0, rx1;
+  f32x4 bacc = {0.0f, 0.0f, 0.0f, 0.0f};
+  const f32x4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto load_row = [&](int64_t m, f32x4& ra, f32x4& rx) {
+    if (m < m1) {
+      ra = a_valid > 0 ? load4_masked(a + m * lda + an, a_valid) : zero4;
+      const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? m : m / x_div);
+      rx = x_valid > 0 ? load4_masked(x + xr * ldx + xk, x_valid) : zero4;
+    } else {
+      ra = zero4;
+      rx = zero4;
+    }
+  };
+  auto load = [&](int64_t mb) {
+    load_row(mb + lr, ra0, rx0);
+    load_row(mb + lr + 8, ra1, rx1);
+  };
+  auto store = [&](int buf) {
+    *reinterpret_cast<f32x4*>(&As[buf][lr][lc]) = ra0;
+    *reinterpret_cast<f32x4*>(&Xs[buf][lr][lc]) = rx0;
+    *reinterpret_cast<f32x4*>(&As[buf][lr + 8][lc]) = ra1;
+    *reinterpret_cast<f32x4*>(&Xs[buf][lr + 8][lc]) = rx1;
+    if (do_bias) bacc += ra0 + ra1;
+  };
+  const bool n_act0 = n0 + 64 * wn < N, n_act1 = n0 + 64 * wn + 32 < N;
+  const bool k_act0 = k0 + 64 * wk < K, k_act1 = k0 + 64 * wk + 32 < K;
+  f32x16 acc00 = f32x16{}, acc01 = f32x16{}, acc10 = f32x16{}, acc11 = f32x16{};
+  const int nstages = (int)((m1 - m0 + kWS - 1) / kWS);
+  load(m0);
+  store(0);
+  __syncthreads();
+  const int h = lane >> 5, c = lane & 31;
+  for (int st = 0; st < nstages; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nstages) load(m0 + (int64_t)kWS * (st + 1));
+    if (n_act0 && k_act0) {
+#pragma unroll
+      for (int ks = 0; ks < kWS / 2; ++ks) {
+        const float* ar = &As[buf][2 * ks + h][64 * wn + c];
+        const float* xr = &Xs[buf][2 * ks + h][64 * wk + c];
+        const float a0 = ar[0], a1 = ar[32], x0 = xr[0], x1 = xr[32];
+        acc00 = mfma32t(a0, x0, acc00);
+        if (k_act1) acc01 = mfma32t(a0, x1, acc01);
+        if (n_act1) acc10 = mfma32t(a1, x0, acc10);
+        if (n_act1 && k_act1) acc11 = mfma32t(a1, x1, acc11);
+      }
+    }
+    if (st + 1 < nstages) store(buf ^ 1);
+    __syncthreads();
+  }
+  const int KP = K + 1;
+  float* out = partial + (size_t)chunk * N * KP;
+  auto emit = [&](const f32x16& acc, int i, int j) {
+    const int kk = k0 + 64 * wk + 32 * j + c;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int nn = n0 + 64 * wn + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (nn < N && kk < K) out[(size_t)nn * KP + kk] = acc[g];
+    }
+  };
+  emit(acc00, 0, 0);
+  emit(acc01, 0, 1);
+  emit(acc10, 1, 0);
+  emit(acc11, 1, 1);
+  if (do_bias) {
+    // the first stage's rows were added in the prologue store; every stage's a rows passed
+    // through store() exactly once
+    *reinterpret_cast<f32x4*>(&bsum[lr][lc]) = bacc;
+    __syncthreads();
+    if (tid < kWT && n0 + tid < N) {
+      float sum = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sum += bsum[r][tid];
+      out[(size_t)(n0 + tid) * KP + K] = sum;
+    }
+  }
+}
+
 // out_w[n][k] (ld K) and out_b[n] (nullable) += / = sum over chunks
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w,
@@ -413,11 +534,22 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
                  float* out_w, float* out_b, int accumulate, float* ws, hipStream_t s) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
-  const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
   const int chunks = (int)((M + kWChunk - 1) / kWChunk);
-  hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N, x,
-                     ldx, K, x_div, M, ws);
-  int rc = check_launch("wgrad_kernel");
+  const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
+  int rc;
+  if (aligned && N >= 32 && K >= 1) {
+    const int ntn = (N + kWT - 1) / kWT, ntk = (K + kWT - 1) / kWT;
+    const int tiles = ntn * ntk;
+    const int blocks = ((chunks + 7) / 8) * 8 * tiles;
+    hipLaunchKernelGGL(wgrad_lds_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div, M, ntk,
+                       tiles, chunks, ws);
+    rc = check_launch("wgrad_lds_kernel");
+  } else {
+    const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N,
+                       x, ldx, K, x_div, M, ws);
+    rc = check_launch("wgrad_kernel");
+  }
   if (rc) return rc;
   const int64_t total = (int64_t)N * KP;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, chunks, N, K,

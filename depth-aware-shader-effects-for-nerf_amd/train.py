@@ -101,7 +101,7 @@ class Trainer:
         return self._ws
 
     # ------------------------------------------------------------------------------ one step
-    def forward_backward(self, rays_o, rays_d, target, app_idx=None, *, t_rand=None, seed=None):
+    def forward_backward(self, rays_o, rays_d, target, app_idx=None, *, t_rand=None, seed=None, _marks=None):
         """Loss (device scalar) and gradients in self.grad for one batch (train.py:77-90).
         rays (B,3) and target (B,3) on the device; app_idx: the batch's image (appearance row).
         t_rand (B,N) = the torch.rand draw of ray_utils.py:80; else the in-kernel RNG on `seed`."""
@@ -132,6 +132,8 @@ class Trainer:
                                           float(self.config.far), N, P(self._tvals[N]), 1, P(t_rand), int(seed),
                                           P(app), rows, P(rgb_map), P(depth), P(ws), ws.numel(), s),
                    "nerf_train_forward")
+        if _marks is not None:
+            _marks[1].record(torch.cuda.current_stream())
         if self.app_grad is not None:
             self.app_grad.zero_()
         dapp = self.dapp if rows else None
@@ -144,6 +146,63 @@ class Trainer:
             self.view(self.grad, 20).zero_()
             self.view(self.grad, 21).zero_()
         return self.loss_buf[0], rgb_map
+
+    def profile_step(self, rays_o, rays_d, target, app_idx=None, seed=12345):
+        """Event-timed phases of one training step through the stage entry points (no parameter
+        update): {phase: ms} for the forward MLP, the MLP data-gradient chain, the weight
+        gradients and the whole forward+backward."""
+        lib, s, P = self.lib, _lib.stream(), _lib.ptr
+        cur = torch.cuda.current_stream()
+        N = self.config.num_samples
+        o = rays_o.reshape(-1, 3).to(self.dev, torch.float32).contiguous()
+        d = rays_d.reshape(-1, 3).to(self.dev, torch.float32).contiguous()
+        tgt = target.reshape(-1, 3).to(self.dev, torch.float32).contiguous()
+        B = o.shape[0]
+        M = B * N
+        dev = self.dev
+        dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
+        feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
+        rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
+        save, grad = torch.empty(M, 2400, device=dev), torch.empty(M, 2308, device=dev)
+        rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
+        dsig, drgb, sq = torch.empty(M, device=dev), torch.empty(M, 3, device=dev), torch.empty(B, device=dev)
+        grads = [torch.empty_like(self.view(self.grad, i)) for i in range(24)]
+        gptr = (ctypes.c_void_p * 24)(*[g.data_ptr() for g in grads])
+        wsz = self.lib.nerf_param_grads_workspace_bytes(M)
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        app, rows = (self.appearance_embeddings[int(app_idx)].reshape(1, _APP_DIM), 1) \
+            if (self.n_images and app_idx is not None) else (None, 0)
+        if N not in self._tvals:
+            self._tvals[N] = linspace_table(N, dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+        ck = _lib.check
+        ev[0].record(cur)
+        ck(lib.nerf_pack_weights(self.param_ptrs, P(self.packed), s), "pack")
+        ck(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), s), "packT")
+        ev[1].record(cur)
+        ck(lib.nerf_normalize_dirs(P(d), B, P(dn), s), "normalize")
+        ck(lib.nerf_sample_stratified(P(o), P(dn), B, float(self.config.near), float(self.config.far), N,
+                                      P(self._tvals[N]), 1, None, seed, P(z), None, s), "stratified")
+        ck(lib.nerf_ray_features_train(P(self.packed), P(dn), B, P(app), rows, P(feat), P(encd), s), "features")
+        ev[2].record(cur)
+        ck(lib.nerf_mlp_forward_train(P(self.packed), P(o), P(dn), P(z), B, N, P(feat), P(encd), P(rgb), P(sigma),
+                                      P(save), s), "mlp_forward_train")
+        ev[3].record(cur)
+        ck(lib.nerf_composite(P(rgb), P(sigma), P(z), B, N, P(rgb_map), P(depth), None, s), "composite")
+        ck(lib.nerf_composite_backward(P(rgb), P(sigma), P(z), P(rgb_map), P(tgt), B, N, 2.0 / (3 * B), P(dsig),
+                                       P(drgb), P(sq), s), "composite_backward")
+        ev[4].record(cur)
+        ck(lib.nerf_mlp_backward(P(self.packed), P(self.packedT), P(save), P(sigma), P(rgb), P(dsig), P(drgb), M,
+                                 P(grad), s), "mlp_backward")
+        ev[5].record(cur)
+        ck(lib.nerf_param_grads(P(save), P(grad), M, N, P(app), rows, P(self.packed), gptr, P(self.dapp), P(ws),
+                                wsz, s), "param_grads")
+        ev[6].record(cur)
+        torch.cuda.synchronize()
+        return {"pack_ms": ev[0].elapsed_time(ev[1]), "rays_ms": ev[1].elapsed_time(ev[2]),
+                "mlp_forward_ms": ev[2].elapsed_time(ev[3]), "composite_fwd_bwd_ms": ev[3].elapsed_time(ev[4]),
+                "mlp_backward_ms": ev[4].elapsed_time(ev[5]), "param_grads_ms": ev[5].elapsed_time(ev[6]),
+                "total_ms": ev[0].elapsed_time(ev[6])}
 
     def all_reduce(self):
         """Average the gradients over the data-parallel group (one RCCL all-reduce)."""

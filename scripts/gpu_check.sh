@@ -20,6 +20,7 @@ for step in "$@"; do
     pytest_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     pytest_train) run pytest_train 600 python -m pytest tests/test_gpu_train.py -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
+    bench_train) run bench_train 600 python bench_train.py --steps 20 --warmup 3 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
