@@ -122,13 +122,14 @@ constexpr int kSaveHd = kSaveRDir + kDirHidden;              // 2272
 constexpr int kSaveRow = kSaveHd + kDirHidden;               // 2400 floats per sample
 
 // Per-sample gradient row written by the backward pass (nerf_mlp_backward):
-//   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dhd (128) | dsigma_pre | drgb_pre (3)]
-// dpre_l = d loss / d (pre-activation of trunk layer l), dhd = d loss / d hd.
+//   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dhd (128) | drgb_pre (3) + pad | dsigma_pre + pad]
+// dpre_l = d loss / d (pre-activation of trunk layer l), dhd = d loss / d hd.  Every slice starts
+// on a 16-byte boundary (the weight-gradient GEMM streams them with 16-byte loads).
 constexpr int kGradDir = 8 * kHidden;                        // 2048
 constexpr int kGradHd = kGradDir + kDirHidden;               // 2176
-constexpr int kGradSigma = kGradHd + kDirHidden;             // 2304
-constexpr int kGradRgb = kGradSigma + 1;                     // 2305
-constexpr int kGradRow = 2308;
+constexpr int kGradRgb = kGradHd + kDirHidden;               // 2304
+constexpr int kGradSigma = kGradRgb + 4;                     // 2308
+constexpr int kGradRow = kGradSigma + 4;                     // 2312
 
 // Float offset, inside matrix m's fragment array, of element j of lane `lane` in the
 // fragment block (n-tile nt, k-step quad kq): ks = 4*kq + j.

@@ -340,14 +340,17 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
 }
 
 // ---------------------------------------------------------------------------------- wgrad
-// partial[c][n][k'] = sum over samples m of chunk c of a[m][n] * x'[m][k'], k' < K + 1, where
-// x'[m][k] = x[xrow(m)][k] for k < K and x'[m][K] = 1 (the bias column).  xrow(m) = m / x_div
-// (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).
-// One wave computes a 32 (n) x 64 (k') tile of one chunk on v_mfma_f32_32x32x2_f32 (two samples
-// per MFMA): A = a^T fragment (lane: n = l&31, sample = l>>5), B = x' fragment (sample = l>>5,
-// k = l&31); loads are 128 contiguous bytes per half-wave.
+// partial[c][n*KP + k'] = sum over samples m of chunk c of a[m][n] * x'[m][k'], k' < KP = K + 1,
+// where x'[m][k] = x[xrow(m)][k] for k < K and x'[m][K] = 1 (the bias column).  xrow(m) = m / x_div
+// (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).  Each chunk's
+// partial occupies wgrad_stride(N, K) floats (N*KP rounded up to 4, for 16-byte reduce loads).
 constexpr int kWChunk = 2048;   // samples per chunk
 
+NERF_HD inline int64_t wgrad_stride(int N, int K) { return (((int64_t)N * (K + 1)) + 3) & ~(int64_t)3; }
+
+// Fallback (unaligned operands): one wave per 32 (n) x 64 (k') tile of one chunk, operands
+// loaded straight from global memory (A = a^T fragment: n = l&31, sample = l>>5; B = x'
+// fragment: sample = l>>5, k = l&31).
 __global__ void __launch_bounds__(256)
 wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
              int64_t x_div, int64_t M, float* __restrict__ partial) {
@@ -367,18 +370,18 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
   // uniform trip count for the whole wave (MFMA is a wave-wide instruction); a sample past the
   // chunk end contributes a zero a-operand
   const int pairs = (int)((m1 - m0 + 1) / 2);
-  const int mlast = (int)m1 - 1;
+  const int64_t mlast = m1 - 1;
   for (int p = 0; p < pairs; ++p) {
-    const int m = (int)m0 + 2 * p + hm;
-    const int mc = m < mlast ? m : mlast;
-    const float av = (n < N && m <= mlast) ? a[(int64_t)mc * lda + n] : 0.0f;
-    const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? mc : mc / (int)x_div);
+    const int64_t m = m0 + 2 * p + hm;
+    const int64_t mc = m < mlast ? m : mlast;
+    const float av = (n < N && m <= mlast) ? a[mc * lda + n] : 0.0f;
+    const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? mc : mc / x_div);
     const float x0 = ka < K ? x[xr * ldx + ka] : (ka == K ? 1.0f : 0.0f);
     const float x1 = kb < K ? x[xr * ldx + kb] : (kb == K ? 1.0f : 0.0f);
     acc0 = mfma32t(av, x0, acc0);
     acc1 = mfma32t(av, x1, acc1);
   }
-  float* out = partial + (size_t)blockIdx.y * N * KP;
+  float* out = partial + (size_t)blockIdx.y * wgrad_stride(N, K);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     const int row = n0 + (g & 3) + 8 * (g >> 2) + 4 * hm;
@@ -389,18 +392,18 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
   }
 }
 
-// The main weight-gradient kernel: a 128 (n) x 128 (k) output tile of one 2048-sample chunk per
-// workgroup, samples streamed through LDS 16 at a time (double-buffered: the next stage's global
-// loads are in flight while the current stage's MFMAs run).  Four waves in a 2 x 2 arrangement,
-// each owning 64 x 64 = 2 x 2 accumulator tiles of v_mfma_f32_32x32x2_f32; per k-step (two
-// samples) a wave reads 4 operand values from LDS for 4 MFMAs.  The bias column (sum over
-// samples of a[m][n]) is accumulated from the staged a values by the k-tile-0 workgroups on the
-// VALU.  Blocks that share a chunk are launched 8 apart, so they land on the same XCD and the
-// chunk's rows are fetched from HBM once per L2 (blockIdx -> XCD is round-robin).
+// The main weight-gradient kernel.  A workgroup computes a (64 WN) x (64 WK) output tile of one
+// 2048-sample chunk (WN * WK = 4 waves, each owning 64 x 64 = 2 x 2 accumulator tiles of
+// v_mfma_f32_32x32x2_f32), streaming the chunk's a and x rows through LDS 16 samples at a time,
+// double-buffered: the next stage's 16-byte global loads are in flight while the current
+// stage's MFMAs run, one barrier per stage.  Per k-step (two samples) a wave reads 4 operand
+// values from LDS for 4 MFMAs; a wave whose n or k range lies past N or K skips its MFMAs.  The
+// bias column (sum over samples of a[m][n]) is accumulated from the staged a values by the
+// k-tile-0 workgroups on the VALU.  Workgroups sharing a chunk are launched 8 apart so they run
+// on the same XCD (blockIdx -> XCD is round-robin) and the chunk's rows come from HBM once per L2.
+// Tile shapes: WN=2, WK=2 (128 x 128) for the 256-wide layers; WN=4, WK=1 (256 x 64) when K <= 64.
 // Preconditions (host-checked): a, x 16-byte aligned, lda % 4 == 0, ldx % 4 == 0.
-constexpr int kWT = 128;       // output tile edge
 constexpr int kWS = 16;        // samples per LDS stage
-constexpr int kWPad = 160;     // LDS row stride in floats (row s+1 lands 32 banks away)
 
 __device__ __forceinline__ f32x4 load4_masked(const float* __restrict__ p, int valid) {
   if (valid >= 4) return *reinterpret_cast<const f32x4*>(p);
@@ -412,49 +415,59 @@ __device__ __forceinline__ f32x4 load4_masked(const float* __restrict__ p, int v
   return v;
 }
 
+template <int WN, int WK>
 __global__ void __launch_bounds__(256, 2)
 wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
                  int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
-  __shared__ float As[2][kWS][kWPad];
-  __shared__ float Xs[2][kWS][kWPad];
-  __shared__ float bsum[8][kWT];
+  static_assert(WN * WK == 4, "four waves");
+  constexpr int BN = 64 * WN, BK = 64 * WK;
+  constexpr int APAD = BN + 32, XPAD = BK + 32;    // row s+1 lands 32 banks away from row s
+  constexpr int AC4 = BN / 4, XC4 = BK / 4;        // float4 columns per staged row
+  __shared__ float As[2][kWS][APAD];
+  __shared__ float Xs[2][kWS][XPAD];
+  __shared__ float bsum[256 / AC4][BN];
   const int b = blockIdx.x;
   const int grp = b / (8 * tiles), rem = b % (8 * tiles);
   const int chunk = grp * 8 + (rem & 7);
   const int tile = rem >> 3;
   if (chunk >= chunks) return;                     // uniform over the block, before any barrier
-  const int n0 = (tile / ntk) * kWT, k0 = (tile % ntk) * kWT;
+  const int n0 = (tile / ntk) * BN, k0 = (tile % ntk) * BK;
   const bool do_bias = (tile % ntk) == 0;
   const int64_t m0 = (int64_t)chunk * kWChunk;
   const int64_t m1 = m0 + kWChunk < M ? m0 + kWChunk : M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wn = w & 1, wk = w >> 1;
-  const int lr = tid >> 5, lc = (tid & 31) * 4;
-  const int an = n0 + lc, xk = k0 + lc;
-  const int a_valid = N - an, x_valid = K - xk;
-  f32x4 ra0, ra1, rx0, rx1;
+  const int wn = w % WN, wk = w / WN;
+  // loader: thread tid moves float4 column tid % C4 of rows tid / C4 + (256 / C4) p
+  const int a_c = (tid % AC4) * 4, a_r = tid / AC4;
+  const int x_c = (tid % XC4) * 4, x_r = tid / XC4;
+  constexpr int AROWS = 256 / AC4, XROWS = 256 / XC4;   // rows per pass
+  const int a_valid = N - (n0 + a_c), x_valid = K - (k0 + x_c);
+  f32x4 ra[WN], rx[WK];
   f32x4 bacc = {0.0f, 0.0f, 0.0f, 0.0f};
   const f32x4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto load_row = [&](int64_t m, f32x4& ra, f32x4& rx) {
-    if (m < m1) {
-      ra = a_valid > 0 ? load4_masked(a + m * lda + an, a_valid) : zero4;
+  auto load = [&](int64_t mb) __attribute__((always_inline)) {
+    sfor<WN>([&](auto pc) __attribute__((always_inline)) {
+      constexpr int p = decltype(pc)::value;
+      const int64_t m = mb + a_r + AROWS * p;
+      ra[p] = (m < m1 && a_valid > 0) ? load4_masked(a + m * lda + n0 + a_c, a_valid) : zero4;
+    });
+    sfor<WK>([&](auto pc) __attribute__((always_inline)) {
+      constexpr int p = decltype(pc)::value;
+      const int64_t m = mb + x_r + XROWS * p;
       const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? m : m / x_div);
-      rx = x_valid > 0 ? load4_masked(x + xr * ldx + xk, x_valid) : zero4;
-    } else {
-      ra = zero4;
-      rx = zero4;
-    }
+      rx[p] = (m < m1 && x_valid > 0) ? load4_masked(x + xr * ldx + k0 + x_c, x_valid) : zero4;
+    });
   };
-  auto load = [&](int64_t mb) {
-    load_row(mb + lr, ra0, rx0);
-    load_row(mb + lr + 8, ra1, rx1);
-  };
-  auto store = [&](int buf) {
-    *reinterpret_cast<f32x4*>(&As[buf][lr][lc]) = ra0;
-    *reinterpret_cast<f32x4*>(&Xs[buf][lr][lc]) = rx0;
-    *reinterpret_cast<f32x4*>(&As[buf][lr + 8][lc]) = ra1;
-    *reinterpret_cast<f32x4*>(&Xs[buf][lr + 8][lc]) = rx1;
-    if (do_bias) bacc += ra0 + ra1;
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    sfor<WN>([&](auto pc) __attribute__((always_inline)) {
+      constexpr int p = decltype(pc)::value;
+      *reinterpret_cast<f32x4*>(&As[buf][a_r + AROWS * p][a_c]) = ra[p];
+      if (do_bias) bacc += ra[p];
+    });
+    sfor<WK>([&](auto pc) __attribute__((always_inline)) {
+      constexpr int p = decltype(pc)::value;
+      *reinterpret_cast<f32x4*>(&Xs[buf][x_r + XROWS * p][x_c]) = rx[p];
+    });
   };
   const bool n_act0 = n0 + 64 * wn < N, n_act1 = n0 + 64 * wn + 32 < N;
   const bool k_act0 = k0 + 64 * wk < K, k_act1 = k0 + 64 * wk + 32 < K;
@@ -483,8 +496,8 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
     __syncthreads();
   }
   const int KP = K + 1;
-  float* out = partial + (size_t)chunk * N * KP;
-  auto emit = [&](const f32x16& acc, int i, int j) {
+  float* out = partial + (size_t)chunk * wgrad_stride(N, K);
+  auto emit = [&](const f32x16& acc, int i, int j) __attribute__((always_inline)) {
     const int kk = k0 + 64 * wk + 32 * j + c;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -497,37 +510,73 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   emit(acc10, 1, 0);
   emit(acc11, 1, 1);
   if (do_bias) {
-    // the first stage's rows were added in the prologue store; every stage's a rows passed
-    // through store() exactly once
-    *reinterpret_cast<f32x4*>(&bsum[lr][lc]) = bacc;
+    // every staged a row passed through store() exactly once (the prologue stores stage 0)
+    *reinterpret_cast<f32x4*>(&bsum[a_r][a_c]) = bacc;
     __syncthreads();
-    if (tid < kWT && n0 + tid < N) {
+    if (tid < BN && n0 + tid < N) {
       float sum = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sum += bsum[r][tid];
+      for (int r = 0; r < AROWS; ++r) sum += bsum[r][tid];
       out[(size_t)(n0 + tid) * KP + K] = sum;
     }
   }
 }
 
-// out_w[n][k] (ld K) and out_b[n] (nullable) += / = sum over chunks
+// out_w[n][k] (ld K) and out_b[n] (nullable) = (accumulate ? out : 0) + sum over chunks, in chunk
+// order.  A workgroup owns 64 float4 columns of the partial layout; its 4 waves each sum a
+// quarter of the chunks (fixed order), then the quarters are added in order: deterministic.
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w,
                     float* __restrict__ out_b, int accumulate) {
+  __shared__ f32x4 part[4][64];
   const int KP = K + 1;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)N * KP) return;
-  double acc = 0.0;
-  for (int c = 0; c < chunks; ++c) acc += (double)partial[(size_t)c * N * KP + idx];
-  const int n = (int)(idx / KP), k = (int)(idx % KP);
-  float* dst = k < K ? out_w + (size_t)n * K + k : (out_b ? out_b + n : nullptr);
-  if (!dst) return;
-  *dst = accumulate ? *dst + (float)acc : (float)acc;
+  const int64_t stride = wgrad_stride(N, K);
+  const int64_t col4 = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  const int per = (chunks + 3) / 4;
+  const int c0 = q * per, c1 = c0 + per < chunks ? c0 + per : chunks;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (col4 * 4 < stride) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(partial) + col4;
+    const int64_t s4 = stride / 4;
+    int c = c0;
+    for (; c + 4 <= c1; c += 4) {
+      const f32x4 v0 = p[(c + 0) * s4], v1 = p[(c + 1) * s4], v2 = p[(c + 2) * s4], v3 = p[(c + 3) * s4];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; c < c1; ++c) acc += p[c * s4];
+  }
+  part[q][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (q != 0 || col4 * 4 >= stride) return;
+  const f32x4 sum = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t idx = col4 * 4 + e;
+    if (idx >= (int64_t)N * KP) break;
+    const int n = (int)(idx / KP), k = (int)(idx % KP);
+    float* dst = k < K ? out_w + (size_t)n * K + k : (out_b ? out_b + n : nullptr);
+    if (dst) *dst = accumulate ? *dst + sum[e] : sum[e];
+  }
 }
 
 size_t wgrad_workspace_floats(int64_t M, int N, int K) {
   const int64_t chunks = (M + kWChunk - 1) / kWChunk;
-  return (size_t)chunks * N * (K + 1);
+  return (size_t)chunks * wgrad_stride(N, K);
+}
+
+template <int WN, int WK>
+static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
+                            int64_t M, int chunks, float* ws, hipStream_t s) {
+  const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
+  const int tiles = ntn * ntk;
+  const int blocks = ((chunks + 7) / 8) * 8 * tiles;
+  hipLaunchKernelGGL((wgrad_lds_kernel<WN, WK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div,
+                     M, ntk, tiles, chunks, ws);
+  return check_launch("wgrad_lds_kernel");
 }
 
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
@@ -537,22 +586,19 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   const int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
   int rc;
-  if (aligned && N >= 32 && K >= 1) {
-    const int ntn = (N + kWT - 1) / kWT, ntk = (K + kWT - 1) / kWT;
-    const int tiles = ntn * ntk;
-    const int blocks = ((chunks + 7) / 8) * 8 * tiles;
-    hipLaunchKernelGGL(wgrad_lds_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div, M, ntk,
-                       tiles, chunks, ws);
-    rc = check_launch("wgrad_lds_kernel");
-  } else {
+  if (aligned && K >= 1 && K <= 64 && N > 64)
+    rc = launch_wgrad_lds<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+  else if (aligned && K >= 1)
+    rc = launch_wgrad_lds<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+  else {
     const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N,
                        x, ldx, K, x_div, M, ws);
     rc = check_launch("wgrad_kernel");
   }
   if (rc) return rc;
-  const int64_t total = (int64_t)N * KP;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ws, chunks, N, K,
+  const int64_t cols4 = wgrad_stride(N, K) / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(256), 0, s, ws, chunks, N, K,
                      out_w, out_b, accumulate);
   return check_launch("wgrad_reduce_kernel");
 }

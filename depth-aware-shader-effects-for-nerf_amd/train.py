@@ -163,7 +163,7 @@ class Trainer:
         dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
         feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save, grad = torch.empty(M, 2400, device=dev), torch.empty(M, 2308, device=dev)
+        save, grad = torch.empty(M, 2400, device=dev), torch.empty(M, 2312, device=dev)
         rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
         dsig, drgb, sq = torch.empty(M, device=dev), torch.empty(M, 3, device=dev), torch.empty(B, device=dev)
         grads = [torch.empty_like(self.view(self.grad, i)) for i in range(24)]

@@ -27,7 +27,7 @@ extern "C" {
 
 /* Per-sample rows the forward saves / the backward writes (floats). */
 #define NERF_SAVE_ROW 2400 /* [h0..h3 | enc_x(64) | h4..h7 | enc_d(32) | r_dir(128) | hd(128)] */
-#define NERF_GRAD_ROW 2308 /* [dpre_0..7 (256 each) | dpre_dir(128) | dhd(128) | dsigma | drgb(3)] */
+#define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dhd(128) | drgb(3)+pad | dsigma+pad] */
 
 /* ---------------------------------------------------------------- whole step
  * Forward of train.py:77-84 (coarse volume_render, n_importance ignored as in

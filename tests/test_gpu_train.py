@@ -103,7 +103,7 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
     feat, encd = torch.empty(R, 256, device=dev), torch.empty(R, 32, device=dev)
     rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
     save = torch.empty(M, 2400, device=dev)
-    grad = torch.empty(M, 2308, device=dev)
+    grad = torch.empty(M, 2312, device=dev)
     s = L.stream()
     L.check(lib.nerf_ray_features_train(L.ptr(packed), L.ptr(dg), R, L.ptr(a), rows, L.ptr(feat), L.ptr(encd), s),
             "feat")
