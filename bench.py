@@ -13,11 +13,16 @@ scaling, 640,000 rays per GPU) and reassembled on every rank with one RCCL all-g
 [r,g,b,depth] per ray.
 Rank 0 prints one JSON line.  value = rays of all ranks / max-over-ranks wall time.
 
-roofline: the dominant kernel is the fused PE->MLP kernel (mlp_kernel).  Its algorithmic
-work is 1,048,832 FLOP per evaluated sample; each step launches it
-twice (B*64 and B*128 samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, the time
+roofline: the dominant kernel is the fused PE->MLP kernel.  Its algorithmic work is 1,048,832
+FLOP per evaluated sample; each step launches it twice (B*64 and B*128
+samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, the time
 measured with HIP events around every launch inside the timed steps (on the stream it runs
-on); peak = the fp32 MFMA dense peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+on).  --arith selects the MLP arithmetic (include/nerfmi.h, nerf_arith), both fp32-accurate:
+  f16x3 (default, mlp16_kernel): every fp32 product is three f16 MFMA products of a hi/lo split;
+        peak = the f16 dense MFMA peak / 3 = 2516.8 / 3 = 838.9 TFLOP/s of fp32-equivalent work
+        (MI355X_MICROARCH.md: f16 = 16x the f32 MFMA rate); "mfma_busy" reports the issued f16
+        MFMA FLOP (3072 v_mfma_f32_32x32x16_f16 per 32 samples) against 2516.8 TFLOP/s;
+  f32   (mlp_kernel): v_mfma_f32_32x32x2_f32, peak 157.3 TFLOP/s.
 cpu_baseline: the oracle (PyTorch-CPU restatement, oracle/nerf_oracle.py) timed on a
 bounded sample of the same workload on this host's cores (rank 0, N=1 only); the GPU renders
 the same rays with the same uniforms and the line reports the PSNR of its rgb against the
@@ -44,6 +49,8 @@ H = W = 800
 N_COARSE, N_FINE = 64, 128
 FLOP_PER_SAMPLE = 1_048_832           # SURVEY.md §8d, DESIGN.md §Roofline
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
+MFMA_F16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # f16/bf16 dense MFMA = 16x the f32 rate
+F16X3_ISSUED_FLOP_PER_SAMPLE = 3072 * 32 * 32 * 16 * 2 // 32   # mlp16_kernel MFMAs per 32-sample wave
 
 
 def parse():
@@ -52,6 +59,7 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="chair")
+    p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="MLP MFMA arithmetic")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
     return p.parse_args()
@@ -95,8 +103,8 @@ def cpu_baseline(target_s, gpu_render=None):
     return out, psnr
 
 
-def pmc_traffic():
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+def pmc_traffic(arith):
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_summary{'_f16x3' if arith == 'f16x3' else ''}.json")))
     if not paths:
         return None, None
     with open(paths[-1]) as f:
@@ -114,6 +122,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import nerfmi
     from nerfmi import cameras, frames
+    nerfmi.set_mlp_arith(args.arith)
 
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
@@ -159,7 +168,13 @@ def main():
         per_kind.setdefault(k, []).append(a.elapsed_time(b))
     if rank == 0:
         total_rays = B * world * args.steps
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic(args.arith)
+        if args.arith == "f16x3":
+            kernel, peak = "nerf::mlp16_kernel", MFMA_F16_PEAK_TFLOPS / 3
+            busy = mlp_samples * F16X3_ISSUED_FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS
+        else:
+            kernel, peak = "nerf::mlp_kernel", MFMA_F32_PEAK_TFLOPS
+            busy = achieved / MFMA_F32_PEAK_TFLOPS
         line = {
             "metric": "rays/sec at 800x800, 64 coarse + 128 fine samples",
             "value": total_rays / elapsed,
@@ -180,8 +195,9 @@ def main():
                        "rays_per_gpu_per_step": B, "n_coarse": N_COARSE, "n_fine": N_FINE,
                        "mlp_evals_per_ray": N_COARSE + N_FINE,
                        "parallelism": f"ray-shard x{world} (one frame per GPU) + RCCL all-gather"},
-            "roofline": {"bound": "mfma", "kernel": "nerf::mlp_kernel", "achieved": achieved,
-                         "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS,
+            "mlp_arith": args.arith,
+            "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved,
+                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "mfma_busy": busy,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "launches": len(timing), "avg_launch_ms": mlp_ms / max(len(timing), 1),
                          "avg_launch_ms_by_pass": {k: sum(v) / len(v) for k, v in per_kind.items()},

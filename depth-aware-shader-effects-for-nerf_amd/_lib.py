@@ -38,6 +38,8 @@ _SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nerf_packed_weights_floats": (ctypes.c_size_t, []),
+    "nerf_set_mlp_arith": (ctypes.c_int, [ctypes.c_int]),
+    "nerf_get_mlp_arith": (ctypes.c_int, []),
     "nerf_pack_weights": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p]),
     "nerf_pack_weights_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "nerf_ray_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
@@ -83,7 +85,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 
@@ -105,6 +107,23 @@ def load():
                                f"{ABI_VERSION}; rebuild it")
         _lib = lib
     return _lib
+
+
+ARITH = {"f32": 0, "f16x3": 1}
+
+
+def set_mlp_arith(name):
+    """Select the MLP's MFMA arithmetic for this process (include/nerfmi.h, nerf_arith):
+    "f16x3" (default; split-f16, fp32-accurate) or "f32" (exact f32 products).  Returns the
+    previous name."""
+    if name not in ARITH:
+        raise ValueError(f"nerfmi: unknown MLP arithmetic {name!r}; expected one of {sorted(ARITH)}")
+    prev = load().nerf_set_mlp_arith(ARITH[name])
+    return {v: k for k, v in ARITH.items()}[prev]
+
+
+def get_mlp_arith():
+    return {v: k for k, v in ARITH.items()}[load().nerf_get_mlp_arith()]
 
 
 def check(rc, what):

@@ -11,6 +11,7 @@
 namespace nerf {
 
 static thread_local char g_err[512] = "";
+int g_mlp_arith = NERF_ARITH_F16X3;
 
 int set_error(int code, const char* fmt, ...) {
   va_list ap;
@@ -21,7 +22,16 @@ int set_error(int code, const char* fmt, ...) {
 }
 
 // ---------------------------------------------------------------------------- packing
-// Value of packed element e (layout.h) from the 24 state_dict tensors.
+// Weight of fragment matrix m (layout.h) at output row `row`, source column `col` (-1 = padding).
+NERF_HD inline float frag_weight(const float* const* P, int m, int row, int col) {
+  if (col < 0) return 0.0f;
+  if (m == 8) return P[P_DIR_W][(size_t)row * (kHidden + kDirEnc) + col];
+  const int layer = (m == kSkipPeMat) ? kSkipLayer : m;
+  const int K = (layer == 0) ? kPosEnc : (layer == kSkipLayer ? kHidden + kPosEnc : kHidden);
+  return P[2 * layer][(size_t)row * K + col];
+}
+
+// Value of packed element e < kF32Floats (the exact-f32 path) from the 24 state_dict tensors.
 NERF_HD inline float pack_value(const float* const* P, size_t e) {
   if (e < kFragFloats) {
     int m = 0;
@@ -32,13 +42,7 @@ NERF_HD inline float pack_value(const float* const* P, size_t e) {
     const size_t blk = rel >> 8;
     const int ksq = frag_ksteps(m) / 4;
     const int nt = (int)(blk / ksq), kq = (int)(blk % ksq);
-    const int col = frag_source_col(m, 4 * kq + j, lane);
-    if (col < 0) return 0.0f;
-    const int row = nt * 32 + (lane & 31);
-    if (m == 8) return P[P_DIR_W][(size_t)row * (kHidden + kDirEnc) + col];
-    const int layer = (m == kSkipPeMat) ? kSkipLayer : m;
-    const int K = (layer == 0) ? kPosEnc : (layer == kSkipLayer ? kHidden + kPosEnc : kHidden);
-    return P[2 * layer][(size_t)row * K + col];
+    return frag_weight(P, m, nt * 32 + (lane & 31), frag_source_col(m, 4 * kq + j, lane));
   }
   if (e < kOffSigmaW) {
     const size_t k = e - kOffBias;
@@ -57,18 +61,95 @@ NERF_HD inline float pack_value(const float* const* P, size_t e) {
   return (e - kOffRgbB < 3) ? P[P_RGB_B][e - kOffRgbB] : 0.0f;
 }
 
+// Number of (row, source column) pairs of fragment matrix m, and the i-th of them.
+NERF_HD inline int frag_src_cols(int m) { return frag_is_pe(m) ? kPosEnc : kHidden; }
+NERF_HD inline float frag_weight_at(const float* const* P, int m, int i) {
+  const int K = frag_src_cols(m);
+  return frag_weight(P, m, i / K, (m == kSkipPeMat ? kHidden : 0) + i % K);
+}
+
+// f16x3 word w (two halves) of the split region, given every matrix's scale s_w.
+NERF_HD inline uint32_t pack16_word(const float* const* P, const float* scale, size_t w) {
+  int i = 0;
+  size_t base = kOff16;
+  while (w + kOff16 >= base + s16_floats(s16_order(i))) base += s16_floats(s16_order(i++));
+  const int m = s16_order(i);
+  const size_t rel = w + kOff16 - base;
+  const int NT = frag_ntiles(m);
+  const int ks = (int)(rel / ((size_t)NT * 512));
+  const int r2 = (int)(rel % ((size_t)NT * 512));
+  const int t = r2 / 512, part = (r2 % 512) / 256, lane = (r2 % 256) / 4, jj = r2 % 4;
+  uint32_t word = 0;
+  for (int k = 0; k < 2; ++k) {
+    const int j = 2 * jj + k;
+    const float v = frag_weight(P, m, t * 32 + (lane & 31), s16_source_col(m, ks, lane >> 5, j)) * scale[m];
+    const _Float16 hi = (_Float16)v;
+    const _Float16 out = part == 0 ? hi : (_Float16)(v - (float)hi);
+    uint16_t bits;
+    memcpy(&bits, &out, 2);
+    word |= (uint32_t)bits << (16 * k);
+  }
+  return word;
+}
+
 struct ParamPtrs { const float* p[P_COUNT]; };
 
 __global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restrict__ packed) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < kPackedFloats) packed[e] = pack_value(P.p, e);
+  if (e < kOff16) packed[e] = e < kF32Floats ? pack_value(P.p, e) : 0.0f;
+}
+
+// One block per fragment matrix: s_w = 2^(14 - e) with max|W| < 2^e, and 1/s_w.
+__global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
+  const int m = blockIdx.x;
+  const int n = frag_ntiles(m) * 32 * frag_src_cols(m);
+  float mx = 0.0f;
+  for (int i = threadIdx.x; i < n; i += 256) mx = fmaxf(mx, fabsf(frag_weight_at(P.p, m, i)));
+  __shared__ float red[256];
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int e = s16_exponent(red[0]);
+    packed[kOffScale16 + m] = ldexpf(1.0f, 14 - e);
+    packed[kOffScale16 + kNumFragMats + m] = ldexpf(1.0f, e - 14);
+  }
+}
+
+__global__ void __launch_bounds__(256) pack16_kernel(ParamPtrs P, float* __restrict__ packed) {
+  const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < kFragFloats)
+    reinterpret_cast<uint32_t*>(packed)[kOff16 + w] = pack16_word(P.p, packed + kOffScale16, w);
 }
 
 int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   ParamPtrs P;
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kPackedFloats + 255) / 256)), dim3(256), 0, s, P, packed);
-  return check_launch("pack_kernel");
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kOff16 + 255) / 256)), dim3(256), 0, s, P, packed);
+  if (int rc = check_launch("pack_kernel")) return rc;
+  hipLaunchKernelGGL(scale16_kernel, dim3(kNumFragMats), dim3(256), 0, s, P, packed);
+  if (int rc = check_launch("scale16_kernel")) return rc;
+  hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((kFragFloats + 255) / 256)), dim3(256), 0, s, P, packed);
+  return check_launch("pack16_kernel");
+}
+
+static void pack_host(const float* const* P, float* packed) {
+  for (size_t e = 0; e < kOff16; ++e) packed[e] = e < kF32Floats ? pack_value(P, e) : 0.0f;
+  float* scale = packed + kOffScale16;
+  for (int i = kOffScale16; i < (int)kPackedFloats; ++i) packed[i] = 0.0f;
+  for (int m = 0; m < kNumFragMats; ++m) {
+    const int n = frag_ntiles(m) * 32 * frag_src_cols(m);
+    float mx = 0.0f;
+    for (int i = 0; i < n; ++i) mx = fmaxf(mx, fabsf(frag_weight_at(P, m, i)));
+    const int e = s16_exponent(mx);
+    scale[m] = ldexpf(1.0f, 14 - e);
+    scale[kNumFragMats + m] = ldexpf(1.0f, e - 14);
+  }
+  uint32_t* words = reinterpret_cast<uint32_t*>(packed);
+  for (size_t w = 0; w < kFragFloats; ++w) words[kOff16 + w] = pack16_word(P, scale, w);
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -85,7 +166,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 3; }
+int nerf_abi_version(void) { return 4; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -148,6 +229,18 @@ int nerf_sample_importance_merge(const float* z_vals, const float* weights, cons
 
 size_t nerf_packed_weights_floats(void) { return kPackedFloats; }
 
+int nerf_set_mlp_arith(int arith) {
+  if (arith != NERF_ARITH_F32 && arith != NERF_ARITH_F16X3) {
+    set_error(NERF_ERR_BAD_ARG, "nerf_set_mlp_arith: unknown arithmetic %d", arith);
+    return -1;
+  }
+  const int prev = g_mlp_arith;
+  g_mlp_arith = arith;
+  return prev;
+}
+
+int nerf_get_mlp_arith(void) { return g_mlp_arith; }
+
 int nerf_pack_weights(const float* const* params, float* packed, nerf_stream_t stream) {
   REQUIRE(params && packed, "nerf_pack_weights: null pointer");
   for (int i = 0; i < P_COUNT; ++i) REQUIRE(params[i], "nerf_pack_weights: parameter %d is null", i);
@@ -157,7 +250,7 @@ int nerf_pack_weights(const float* const* params, float* packed, nerf_stream_t s
 int nerf_pack_weights_host(const float* const* params, float* packed) {
   REQUIRE(params && packed, "nerf_pack_weights_host: null pointer");
   for (int i = 0; i < P_COUNT; ++i) REQUIRE(params[i], "nerf_pack_weights_host: parameter %d is null", i);
-  for (size_t e = 0; e < kPackedFloats; ++e) packed[e] = pack_value(params, e);
+  pack_host(params, packed);
   return NERF_OK;
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <utility>
 #include "../../include/nerfmi_train.h"
 #include "layout.h"
 
@@ -19,6 +20,18 @@ inline int check_launch(const char* what) {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, fully expanded by the
+// front end (the loop unroller gives up on bodies this large and would leave the register
+// arrays runtime-indexed, i.e. in scratch).
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
 
@@ -47,6 +60,9 @@ int launch_importance(const float* o, const float* d, const float* z, const floa
 int launch_pack(const float* const* params, float* packed, hipStream_t s);
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
                         int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
+extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
+int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
+                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
                int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
                hipStream_t s, float* save = nullptr, const float* encd = nullptr);

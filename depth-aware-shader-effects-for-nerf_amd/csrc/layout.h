@@ -65,7 +65,34 @@ constexpr size_t kOffAppW = kOffDirWd + kDirHidden * kDirEnc;   // appearance_pr
 constexpr size_t kOffAppB = kOffAppW + kDirHidden * kAppDim;    // appearance_projection.bias (128)
 constexpr size_t kOffRgbW = kOffAppB + kDirHidden;              // rgb_linear.weight (3 x 128)
 constexpr size_t kOffRgbB = kOffRgbW + 3 * kDirHidden;          // rgb_linear.bias (3, padded 4)
-constexpr size_t kPackedFloats = kOffRgbB + 4;
+constexpr size_t kF32Floats = kOffRgbB + 4;                     // end of the exact-f32 path's data
+
+// ---- split-f16 ("f16x3") fragments: the same 10 matrices as f16 hi/lo pairs --------------------
+// The f16x3 MLP runs every dense layer on v_mfma_f32_32x32x16_f16 as three products
+// hi(W)hi(a) + hi(W)lo(a) + lo(W)hi(a), where x*s = hi + lo + O(2^-24 x*s) with hi = f16(x*s)
+// and lo = f16(x*s - hi), s a power of two (per matrix for W, per sample for a) that puts the
+// largest value just under 2^15.  The dropped lo*lo term is O(2^-24): fp32-level accuracy at
+// 3 x 32 MFMA cycles per 16-deep k-step against 8 x 64 for the exact f32 instruction.
+//
+// A k-step is 16 inputs; lane l supplies 8 of them, k = 8(l>>5) + j (j = 0..7), for row or
+// column l&31.  Activation k-step ks = 2t + s reads registers 8s..8s+7 of the previous layer's
+// accumulator tile t as they stand, so element j of lane half h is input feature
+// 32t + 16s + 8(j>>2) + 4h + (j&3).  PE k-step q reads PE slot p = 8q + j (pe_feature).
+//
+// The weights are stored in the order the kernel streams them: matrices in network order
+// (layer 0, 1, 2, 3, 4's activation part, 4's PE part, 5, 6, 7, dir_linear's h part), each as
+// k-step "chunks" of NT tiles x {hi, lo} "pieces" of 64 lanes x 8 halves (1 KiB).
+NERF_HD constexpr int s16_order(int i) { return i < 5 ? i : (i == 5 ? kSkipPeMat : i - 1); }
+NERF_HD constexpr int s16_ksteps(int m) { return frag_ksteps(m) / 8; }             // 16-deep k-steps
+NERF_HD constexpr size_t s16_floats(int m) { return (size_t)frag_ntiles(m) * s16_ksteps(m) * 512; }
+constexpr size_t kOff16 = (kF32Floats + 255) / 256 * 256;                  // 1 KiB aligned
+NERF_HD constexpr size_t s16_offset(int m) {
+  size_t off = kOff16;
+  for (int i = 0; s16_order(i) != m; ++i) off += s16_floats(s16_order(i));
+  return off;
+}
+constexpr size_t kOffScale16 = kOff16 + kFragFloats;          // s_w[10] then 1/s_w[10] (pad 32)
+constexpr size_t kPackedFloats = kOffScale16 + 32;
 
 // Index of a state_dict tensor in the 24-pointer parameter list of nerf_pack_weights.
 enum Param {
@@ -102,6 +129,27 @@ NERF_HD inline int frag_source_col(int m, int ks, int lane) {
   const int f = pe_feature(ks - act, h);
   if (f < 0) return -1;
   return (m == kSkipPeMat ? kHidden : 0) + f;   // skip layer input is cat[h, enc_x] (models.py:131)
+}
+
+// Input feature of element j of k-step ks (lane half h) of f16 matrix m, or -1 for padding.
+NERF_HD inline int s16_source_col(int m, int ks, int h, int j) {
+  if (!frag_is_pe(m)) {
+    const int t = ks >> 1, s = ks & 1;
+    return 32 * t + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+  }
+  const int f = pe_feature(8 * ks + j, h);
+  if (f < 0) return -1;
+  return (m == kSkipPeMat ? kHidden : 0) + f;
+}
+
+// Power-of-two scale that maps |x| <= m to |x*s| < 2^14 (so f16 rounding stays under 2^15).
+NERF_HD inline int s16_exponent(float m) {
+  int e = 0;
+  float v = m;
+  if (!(v > 0.0f)) return 0;
+  while (v >= 1.0f && e < 200) { v *= 0.5f; ++e; }
+  while (v < 0.5f && e > -200) { v *= 2.0f; --e; }
+  return e;   // m = v * 2^e, v in [0.5, 1): m < 2^e
 }
 
 }  // namespace nerf

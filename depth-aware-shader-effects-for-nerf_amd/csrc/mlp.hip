@@ -22,8 +22,6 @@
 //
 // Bound: MFMA.  1,048,832 algorithmic FLOP per sample; the kernel
 // issues 8,192 MFMAs of 4,096 FLOP per 32 samples (63->64 and 319->320 input padding).
-#include <utility>
-
 #include "common.h"
 
 namespace nerf {
@@ -60,18 +58,6 @@ __device__ __forceinline__ f32x16 load_rows(const float* __restrict__ v, int nt,
     out[4 * q + 3] = t[3];
   }
   return out;
-}
-
-// Compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, fully expanded by the
-// front end (the loop unroller gives up on bodies this large and would leave the register
-// arrays runtime-indexed, i.e. in scratch).
-template <typename F, int... Is>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 #ifndef NERF_MLP_WAVES
@@ -362,6 +348,8 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
                float* save, const float* encd) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
+  if (!save && g_mlp_arith == NERF_ARITH_F16X3)
+    return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s);
   constexpr int per_block = 32 * NERF_MLP_WAVES;
   const int64_t blocks = (M + per_block - 1) / per_block;
   if (save)

@@ -113,8 +113,22 @@ int nerf_pack_weights_host(const float* const* params, float* packed);
 int nerf_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
                       int64_t app_rows, float* feat, nerf_stream_t stream);
 
+/* ------------------------------------------------------ MLP arithmetic
+ * The MLP's dense layers run on one of two MFMA arithmetics (process-wide,
+ * default NERF_ARITH_F16X3); both give fp32-level results:
+ *   NERF_ARITH_F32   v_mfma_f32_32x32x2_f32: exact f32 products, 157 TFLOP/s peak.
+ *   NERF_ARITH_F16X3 v_mfma_f32_32x32x16_f16 on a hi/lo f16 split of
+ *                    power-of-two-scaled operands, three products per k-step
+ *                    (hi.hi + hi.lo + lo.hi): split residual and dropped term
+ *                    O(2^-24), f32 accumulation; 5.3x the f32 MFMA rate.
+ * nerf_set_mlp_arith returns the previous setting (or -1 for an unknown one). */
+enum nerf_arith { NERF_ARITH_F32 = 0, NERF_ARITH_F16X3 = 1 };
+int nerf_set_mlp_arith(int arith);
+int nerf_get_mlp_arith(void);
+
 /* ----------------------------------------------- R4+R6 fused PE -> NeRF MLP
- * NeRF.forward (src/models.py:105-162) for M = R*N samples, fp32 MFMA.
+ * NeRF.forward (src/models.py:105-162) for M = R*N samples on MFMA
+ * (nerf_set_mlp_arith).
  * With z_vals non-null sample s of ray r sits at pts = origins[r] + dirs[r]*z[r*N+s]
  * (src/ray_utils.py:86); with z_vals null the (R,3) `origins` ARE the points
  * (N must be 1).  ray_feat: (R,256) from nerf_ray_features.  Outputs rgb (M,3),

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box validation: each step under its own time limit; stops at the first crash/abort/timeout
 # (status >= 124), continues past ordinary test failures.  Usage: scripts/gpu_check.sh step...
-#   steps: variants | pytest | pytest_train | bench | smoke
+#   steps: variants | pytest | pytest_all | parity | pytest_train | bench | bench_f32 | bench_train | smoke
 mkdir -p gpurun_out
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -20,6 +20,8 @@ for step in "$@"; do
     pytest_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     pytest_train) run pytest_train 600 python -m pytest tests/test_gpu_train.py -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
+    bench_f32) run bench_f32 600 python bench.py --steps 3 --warmup 1 --arith f32 --no-cpu-baseline ;;
+    parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bench_train) run bench_train 600 python bench_train.py --steps 20 --warmup 3 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -170,6 +170,146 @@ def test_emulated_kernel_matches_oracle(ref_state, app_vec):
         rgb_o, sigma_o = O.nerf_forward(ref_state, x, d, app)
         np.testing.assert_allclose(rgb, rgb_o.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(sigma, sigma_o.numpy(), rtol=1e-4, atol=1e-6)
+
+
+# ---- the split-f16 ("f16x3") region of the packed buffer (layout.h, csrc/mlp16.hip)
+S16_ORDER = (0, 1, 2, 3, 4, 9, 5, 6, 7, 8)
+
+
+def s16_ksteps(m):
+    return frag_ksteps(m) // 8
+
+
+def s16_offset(m):
+    off = (frag_offset(10) + 8 * 256 + 256 + 4 + 128 + 128 * 27 + 128 * 32 + 128 + 384 + 4 + 255) // 256 * 256
+    for i in S16_ORDER:
+        if i == m:
+            return off
+        off += frag_ntiles(i) * s16_ksteps(i) * 512
+
+
+def s16_source_col(m, ks, h, j):
+    if m not in (0, 9):
+        t, s = divmod(ks, 2)
+        return 32 * t + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3)
+    f = pe_feature(8 * ks + j, h)
+    return f if f < 0 else (256 if m == 9 else 0) + f
+
+
+def s16_matrix(packed, m):
+    """(hi, lo, s_w) of matrix m as [n][k], k = 16 ks + 8 h + j (the kernel's k order)."""
+    nt, ks = frag_ntiles(m), s16_ksteps(m)
+    off = s16_offset(m)
+    raw = packed[off: off + nt * ks * 512].view(np.float16).reshape(ks, nt, 2, 2, 32, 8)
+    # [ks][t][part][h][n%32][j] -> [part][t][n%32][ks][h][j]
+    w = raw.transpose(2, 1, 4, 0, 3, 5).reshape(2, nt * 32, ks * 16).astype(np.float64)
+    return w[0], w[1]
+
+
+def s16_scales(packed):
+    base = s16_offset(0) + frag_offset(10)
+    return packed[base: base + 10].astype(np.float64), packed[base + 10: base + 20].astype(np.float64)
+
+
+def s16_cols(m):
+    return [s16_source_col(m, ks, h, j) for ks in range(s16_ksteps(m)) for h in range(2) for j in range(8)]
+
+
+def test_split_f16_fragments_reconstruct_the_weights(ref_state):
+    packed = host_pack(ref_state)
+    s_w, inv_w = s16_scales(packed)
+    assert np.all(s_w * inv_w == 1.0)
+    W = {m: ref_state[f"pts_linears.{m}.weight"].numpy().astype(np.float64) for m in range(8)}
+    W[8] = ref_state["dir_linear.weight"].numpy().astype(np.float64)
+    W[9] = W[4]
+    for m in range(10):
+        hi, lo = s16_matrix(packed, m)
+        src = W[m] if m != 9 else W[4]
+        cols = s16_cols(m)
+        ref = np.stack([src[:, c] if c >= 0 else np.zeros(src.shape[0]) for c in cols], 1)
+        mx = np.abs(ref).max()
+        assert mx * s_w[m] < 2.0 ** 14 and mx * s_w[m] >= 2.0 ** 13, m      # scale puts the max just under 2^14
+        assert np.array_equal(hi, (ref * s_w[m]).astype(np.float32).astype(np.float16).astype(np.float64)), m
+        err = np.abs((hi + lo) * inv_w[m] - ref).max()
+        assert err <= mx * 2.0 ** -23, (m, err)
+
+
+def emulate_forward_f16x3(packed, x, d, app):
+    """csrc/mlp16.hip's dataflow on the host-packed buffer: per-sample power-of-two scales, f16
+    hi/lo split in float32, the three products accumulated in float64."""
+    s_w, inv_w = s16_scales(packed)
+    f32 = np.float32
+
+    def split(v):
+        v = v.astype(f32)
+        hi = v.astype(np.float16)
+        lo = (v - hi.astype(f32)).astype(np.float16)
+        return hi.astype(np.float64), lo.astype(np.float64)
+
+    def scale_of(mx):
+        e = np.frexp(mx.astype(f32))[1]
+        return np.ldexp(1.0, 14 - e)
+
+    def dense(m, a_cols, s):
+        hi, lo = s16_matrix(packed, m)
+        ah, al = split(a_cols * s[:, None])
+        return ah @ hi.T + al @ hi.T + ah @ lo.T
+
+    enc = O.positional_encoding(torch.from_numpy(x), 10).numpy().astype(np.float64)
+    pe_cols = np.stack([enc[:, c] if c >= 0 else np.zeros(len(x)) for c in s16_cols(0)], 1)
+    m_pe = np.maximum(1.0, np.abs(x).max(1).astype(np.float64))
+    off_bias = frag_offset(10)
+    bias = packed[off_bias: off_bias + 8 * 256].reshape(8, 256).astype(np.float64)
+    s = scale_of(m_pe)
+    y = dense(0, pe_cols, s) / (s_w[0] * s)[:, None] + bias[0]
+    for m in range(1, 8):
+        h = np.maximum(y, 0)
+        mx = h.max(1)
+        if m == 4:
+            mx = np.maximum(mx, m_pe)
+        s = scale_of(mx)
+        acc = dense(m, h[:, s16_cols(m)], s)
+        if m == 4:
+            acc += dense(9, np.stack([enc[:, c - 256] if c >= 0 else np.zeros(len(x)) for c in s16_cols(9)], 1), s)
+        y = acc / (s_w[m] * s)[:, None] + bias[m]
+    h = np.maximum(y, 0)
+    p = packed.astype(np.float64)
+    off_sw = off_bias + 8 * 256
+    off_sb = off_sw + 256
+    off_db = off_sb + 4
+    off_dwd = off_db + 128
+    off_aw = off_dwd + 128 * 27
+    off_ab = off_aw + 128 * 32
+    off_rw = off_ab + 128
+    off_rb = off_rw + 3 * 128
+    sigma = np.maximum(h @ p[off_sw: off_sw + 256] + p[off_sb], 0)
+    s = scale_of(h.max(1))
+    encd = O.positional_encoding(torch.from_numpy(d), 4).numpy().astype(np.float64)
+    dvec = p[off_db: off_db + 128] + encd @ p[off_dwd: off_dwd + 128 * 27].reshape(128, 27).T
+    appf = np.zeros(128) if app is None else p[off_ab: off_ab + 128] + app.astype(np.float64) @ \
+        p[off_aw: off_aw + 128 * 32].reshape(128, 32).T
+    hd = np.maximum(dense(8, h[:, s16_cols(8)], s) / (s_w[8] * s)[:, None] + dvec, 0) + appf
+    rgb = 1 / (1 + np.exp(-(hd @ p[off_rw: off_rw + 384].reshape(3, 128).T + p[off_rb: off_rb + 3])))
+    return rgb, sigma[:, None]
+
+
+def test_emulated_f16x3_kernel_matches_oracle(ref_state, app_vec):
+    """The split arithmetic is fp32-accurate: the emulated f16x3 dataflow sits within the
+    parity tolerance of the oracle (and, per element, as close to a float64 evaluation as fp32)."""
+    packed = host_pack(ref_state)
+    torch.manual_seed(5)
+    x = torch.randn(256, 3) * 2
+    d = torch.nn.functional.normalize(torch.randn(256, 3), dim=-1)
+    st64 = {k: v.double() for k, v in ref_state.items()}
+    for app in (None, app_vec):
+        rgb, sigma = emulate_forward_f16x3(packed, x.numpy(), d.numpy(), None if app is None else app.numpy())
+        rgb_o, sigma_o = O.nerf_forward(ref_state, x, d, app)
+        np.testing.assert_allclose(rgb, rgb_o.numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(sigma, sigma_o.numpy(), rtol=1e-4, atol=1e-6)
+        rgb64, _ = O.nerf_forward(st64, x.double(), d.double(), None if app is None else app.double())
+        e16 = np.abs(rgb - rgb64.numpy()).max()
+        e32 = np.abs(rgb_o.double().numpy() - rgb64.numpy()).max()
+        assert e16 <= 4 * e32 + 1e-7, (e16, e32)
 
 
 def host_pack_transposed(state):

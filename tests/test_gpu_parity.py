@@ -36,6 +36,14 @@ def nerfmi_mod():
     return nerfmi
 
 
+@pytest.fixture(scope="module", autouse=True, params=["f16x3", "f32"])
+def arith(request, nerfmi_mod):
+    """Every parity test runs under both MLP arithmetics (include/nerfmi.h, nerf_arith)."""
+    prev = nerfmi_mod.set_mlp_arith(request.param)
+    yield request.param
+    nerfmi_mod.set_mlp_arith(prev)
+
+
 @pytest.fixture(scope="module")
 def model(nerfmi_mod, ref_state):
     m = nerfmi_mod.NeRF(nerfmi_mod.Config())
@@ -105,6 +113,26 @@ def test_forward_matches_reference(nerfmi_mod, model, golden, app_vec):
             assert rgb.shape == (n, 3) and sigma.shape == (n, 1)
             close(rgb, f2[f"rgb_{name}"], what=f"rgb {name}")
             close(sigma, f2[f"sigma_{name}"], what=f"sigma {name}")
+
+
+def test_forward_accuracy_vs_float64(model, ref_state, app_vec, arith):
+    """Both arithmetics are fp32-accurate: max error against a float64 evaluation of the same
+    weights stays within a small multiple of the fp32 CPU path's own error."""
+    torch.manual_seed(12)
+    x = torch.rand(8192, 3) * 6 - 3
+    d = torch.nn.functional.normalize(torch.randn(8192, 3), dim=-1)
+    st64 = {k: v.double() for k, v in ref_state.items()}
+    with torch.no_grad():
+        rgb, sigma = model(x.cuda(), d.cuda(), app_vec.cuda())
+        rgb32, sigma32 = O.nerf_forward(ref_state, x, d, app_vec)
+        rgb64, sigma64 = O.nerf_forward(st64, x.double(), d.double(), app_vec.double())
+    e_gpu = (rgb.cpu().double() - rgb64).abs().max().item()
+    e_cpu = (rgb32.double() - rgb64).abs().max().item()
+    s_gpu = ((sigma.cpu().double() - sigma64).abs() / (sigma64.abs() + 1e-3)).max().item()
+    s_cpu = ((sigma32.double() - sigma64).abs() / (sigma64.abs() + 1e-3)).max().item()
+    print(f"{arith}: rgb max err vs f64 {e_gpu:.3g} (cpu f32 {e_cpu:.3g}); sigma {s_gpu:.3g} (cpu {s_cpu:.3g})")
+    assert e_gpu <= 4 * e_cpu + 1e-7
+    assert s_gpu <= 4 * s_cpu + 1e-6
 
 
 def test_forward_ragged_and_position_independent(model, ref_state):
