@@ -32,6 +32,21 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kW16Waves = 4;           // waves per workgroup, one per SIMD; they share the weight stream
 
+#ifdef NERF_MLP16_STAMPS   // diagnostic build (scripts/microbench/mlp16_stamps.hip): per-wave segment clocks
+__device__ unsigned long long nerf16_stamps[65536][24];
+#define STAMP16(i)                                                                          \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long t_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const int64_t w_ = (int64_t)blockIdx.x * kW16Waves + wave;                              \
+    if (w_ < 65536 && lane == 0) nerf16_stamps[w_][i] = t_;                                 \
+  } while (0)
+#else
+#define STAMP16(i) do {} while (0)
+#endif
+
 struct Operand {                       // B operand of one 16-deep k-step, split
   h16x8 hi, lo;
 };
@@ -56,54 +71,136 @@ __device__ __forceinline__ void split_into(float x, Operand& op, int j) {
 }
 
 // ---- the shared weight stream ------------------------------------------------------------
-// A chunk is NT*2 pieces of 256 floats (64 lanes x 16 B); wave w moves pieces w, w+4, ...
+// LDS (one __shared__ array: a second object can make hipcc drain the DMA before every ds_read):
+//   [ring: 4 slots x 16 KiB][PE: 4 waves x 32 x 64 floats]
+//   [trunk biases 8 x 256 | density_head weight 256, bias 4 | 1/s_w of the 10 matrices, pad 16]
+// (every small vector the layers read sits in LDS: an ordinary global load used while a DMA is in
+// flight makes hipcc wait vmcnt(0), draining the stream)
+constexpr int kSlotFloats = 4096;
+constexpr int kLdsPe = 4 * kSlotFloats;
+constexpr int kLdsBias = kLdsPe + kW16Waves * kPeSteps * 64;
+constexpr int kLdsSigmaW = kLdsBias + 8 * kHidden;
+constexpr int kLdsVecFloats = 8 * kHidden + kHidden + 4;    // kOffBias .. kOffSigmaB + 4, contiguous in `packed`
+constexpr int kLdsScaleInv = kLdsBias + kLdsVecFloats;
+constexpr int kLdsFloats = kLdsScaleInv + 16;               // 105 KiB
+static_assert(kOffSigmaW == kOffBias + 8 * kHidden && kOffSigmaB == kOffSigmaW + kHidden, "packed vector order");
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// A chunk (one 16-deep k-step of NT tiles) is 2*NT pieces of 256 floats (64 lanes x 16 B); wave w
+// moves pieces w, w+4, ... straight into its LDS slot with global_load_lds_dwordx4 (no registers).
 template <int NT>
-__device__ __forceinline__ void chunk_load(f32x4 (&st)[4], const float* __restrict__ chunk, int wave, int lane) {
-  const f32x4* __restrict__ src = reinterpret_cast<const f32x4*>(chunk);
+__device__ __forceinline__ void chunk_dma(const float* __restrict__ chunk, float* slot, int wave, int lane) {
+#ifdef NERF16_T_NODMA
+  return;
+#endif
 #pragma unroll
-  for (int i = 0; i < 2 * NT / kW16Waves; ++i) st[i] = src[(wave + kW16Waves * i) * 64 + lane];
+  for (int i = 0; i < 2 * NT / kW16Waves; ++i) {
+    const int p = wave + kW16Waves * i;
+    __builtin_amdgcn_global_load_lds((gptr_t)(chunk + p * 256 + lane * 4), (lptr_t)(slot + p * 256), 16, 0, 0);
+  }
 }
-template <int NT>
-__device__ __forceinline__ void chunk_store(const f32x4 (&st)[4], f32x4* slot, int wave, int lane) {
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// A fragments of half a chunk (tiles HALF*NT/2 ..), hi and lo per tile.
+template <int NT, int HALF>
+__device__ __forceinline__ void read_half(const float* slot, h16x8 (&a)[4][2], int lane) {
+#ifdef NERF16_T_NOREAD
 #pragma unroll
-  for (int i = 0; i < 2 * NT / kW16Waves; ++i) slot[(wave + kW16Waves * i) * 64 + lane] = st[i];
+  for (int i = 0; i < NT / 2; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
+  return;
+#endif
+#pragma unroll
+  for (int i = 0; i < NT / 2; ++i) {
+    const int t = HALF * (NT / 2) + i;
+    a[i][0] = __builtin_bit_cast(h16x8, *reinterpret_cast<const f32x4*>(slot + (2 * t) * 256 + lane * 4));
+    a[i][1] = __builtin_bit_cast(h16x8, *reinterpret_cast<const f32x4*>(slot + (2 * t + 1) * 256 + lane * 4));
+  }
+}
+
+template <int NT, int HALF, bool FIRST>
+__device__ __forceinline__ void mfma_half(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8]) {
+#ifdef NERF16_T_NOMFMA   // timing-only builds (scripts/microbench/mlp16_stamps.hip); wrong results
+#pragma unroll
+  for (int i = 0; i < NT / 2; ++i)
+    asm volatile("" : "+v"(acc[HALF * (NT / 2) + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
+  return;
+#endif
+  static_for<NT / 2>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    constexpr int t = HALF * (NT / 2) + i;
+    f32x16 c;
+    if constexpr (FIRST) c = mfma16(a[i][1], b.hi, f32x16{});
+    else c = mfma16(a[i][1], b.hi, acc[t]);
+    c = mfma16(a[i][0], b.lo, c);
+    acc[t] = mfma16(a[i][0], b.hi, c);
+  });
+}
+
+// DMA instructions one wave issues for chunk j of a layer with KS chunks of NT tiles followed by
+// a matrix of NEXT_NT tiles (0: the stream ends).
+template <int NT, int KS, int NEXT_NT>
+__device__ __forceinline__ constexpr int dma_per_wave(int j) {
+  return j < KS ? 2 * NT / kW16Waves : 2 * NEXT_NT / kW16Waves;
+}
+
+// Half a k-step: the MFMAs of tiles HALF*NT/2 .. from the fragments in `am`, interleaved with
+// the reads of the next half's fragments into `ar` (RT tiles' worth, from `slot_r`; 0 = none):
+// 2 ds_read_b128 between consecutive tiles' 3 MFMAs, so the LDS latency hides under them.
+template <int NT, int HALF, bool FIRST, int RT, int RHALF>
+__device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
+                                          const float* slot_r, h16x8 (&ar)[4][2], int lane) {
+  if constexpr (RT > 0) read_half<RT, RHALF>(slot_r, ar, lane);
+  mfma_half<NT, HALF, FIRST>(am, b, acc);
+  static_for<NT / 2>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (i < RT / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                            // 3 MFMAs
+  });
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // One dense layer: NT output tiles, KS_ACT activation k-steps from `in` then KS_PE PE k-steps
 // from `pe`, weights at `wm` (stream order; layer 4's PE part follows its activation part).
-// On entry LDS slot 0 holds chunk 0 and st[1] chunk 1; on exit the same holds for `next`
-// (NEXT_NT tiles; 0 = last matrix).  acc is overwritten (the first k-step starts from 0).
+// Pipeline per k-step ks (chunk ks sits in LDS slot ks&3):
+//   MFMA half 0, reading half 1's A | wait own DMA of chunk ks+1, barrier | DMA chunk ks+3 into
+//   the slot chunk ks-1 used | MFMA half 1, reading chunk ks+1's half-0 A
+// On entry chunk 0 is published, chunks 1-2 are in flight and a0 holds chunk 0's half 0; on exit
+// the same holds for `next` (NEXT_NT tiles; 0 = last matrix).
 template <int NT, int KS_ACT, int KS_PE, int NEXT_NT>
-__device__ __forceinline__ void dense16(const float* __restrict__ wm, const float* __restrict__ next,
-                                        f32x4 (&st)[2][4], f32x4 (*ring)[16 * 64], const Operand (&in)[16],
+__device__ __forceinline__ void dense16(const float* __restrict__ wm, const float* __restrict__ next, float* lds,
+                                        h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand (&in)[16],
                                         const Operand (&pe)[4], f32x16 (&acc)[8], int wave, int lane) {
   constexpr int KS = KS_ACT + KS_PE;
-  static_assert(KS % 2 == 0 && KS >= 2, "chunks alternate LDS slots within a matrix");
+  static_assert(KS % 4 == 0, "every matrix starts on LDS slot 0");
   static_for<KS>([&](auto kc) __attribute__((always_inline)) {
     constexpr int ks = decltype(kc)::value;
-    // publish chunk ks+1 (loaded during the previous step) into the slot chunk ks-1 used
-    if constexpr (ks + 1 < KS) chunk_store<NT>(st[(ks + 1) & 1], ring[(ks + 1) & 1], wave, lane);
-    else if constexpr (NEXT_NT > 0) chunk_store<NEXT_NT>(st[(ks + 1) & 1], ring[(ks + 1) & 1], wave, lane);
-    // fetch chunk ks+2 into the registers just freed
-    if constexpr (ks + 2 < KS) chunk_load<NT>(st[ks & 1], wm + (size_t)(ks + 2) * NT * 512, wave, lane);
-    else if constexpr (NEXT_NT > 0)
-      chunk_load<NEXT_NT>(st[ks & 1], next + (size_t)(ks + 2 - KS) * NEXT_NT * 512, wave, lane);
     const Operand& b = [&]() -> const Operand& {
       if constexpr (ks < KS_ACT) return in[ks];
       else return pe[ks - KS_ACT];
     }();
-    const f32x4* slot = ring[ks & 1];
-    static_for<NT>([&](auto tc) __attribute__((always_inline)) {
-      constexpr int t = decltype(tc)::value;
-      const h16x8 ahi = __builtin_bit_cast(h16x8, slot[(2 * t) * 64 + lane]);
-      const h16x8 alo = __builtin_bit_cast(h16x8, slot[(2 * t + 1) * 64 + lane]);
-      f32x16 c;
-      if constexpr (ks == 0) c = mfma16(alo, b.hi, f32x16{});
-      else c = mfma16(alo, b.hi, acc[t]);
-      c = mfma16(ahi, b.lo, c);
-      acc[t] = mfma16(ahi, b.hi, c);
-    });
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): a0's reads (interleaved in the last half-step) are in
+    half_step<NT, 0, ks == 0, NT, 1>(a0, b, acc, lds + (ks & 3) * kSlotFloats, a1, lane);
+    constexpr bool has1 = ks + 1 < KS || NEXT_NT > 0;
+    constexpr bool has2 = ks + 2 < KS || NEXT_NT > 0;
+    constexpr bool has3 = ks + 3 < KS || NEXT_NT > 0;
+#ifndef NERF16_T_NOBARRIER
+    if constexpr (has1) {
+      wait_vmcnt<has2 ? dma_per_wave<NT, KS, NEXT_NT>(ks + 2) : 0>();
+      __builtin_amdgcn_s_barrier();
+    }
+#endif
+    if constexpr (ks + 3 < KS) chunk_dma<NT>(wm + (size_t)(ks + 3) * NT * 512, lds + ((ks + 3) & 3) * kSlotFloats, wave, lane);
+    else if constexpr (has3)
+      chunk_dma<NEXT_NT>(next + (size_t)(ks + 3 - KS) * NEXT_NT * 512, lds + ((ks + 3) & 3) * kSlotFloats, wave, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // a1's reads are in
+    constexpr int RT = ks + 1 < KS ? NT : NEXT_NT;
+    half_step<NT, 1, ks == 0, RT, 0>(a1, b, acc, lds + ((ks + 1) & 3) * kSlotFloats, a0, lane);
   });
 }
 
@@ -150,9 +247,10 @@ __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
              const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
              float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
-  __shared__ f32x4 ring[2][16 * 64];                    // 2 x 16 KiB weight chunks
-  __shared__ float pe_lds[kW16Waves][kPeSteps][64];     // each wave's PE, re-read by the skip layer
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
+
+  STAMP16(0);
   const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
   // every wave runs to the end (the weight stream has barriers); tail lanes repeat sample M-1
   const bool valid = s0 + (lane & 31) < M;
@@ -169,6 +267,18 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
     for (int c = 0; c < 3; ++c) x[c] = orig[3 * s + c];
   }
+  // small vectors into LDS, then the weight stream starts: chunks 0-2 of layer 0 in flight while
+  // the PE is computed (every ordinary load retired first: hipcc waits vmcnt(0) at the use of an
+  // ordinary load while a DMA is in flight)
+  for (int i = threadIdx.x; i < kLdsVecFloats / 4; i += 64 * kW16Waves)
+    reinterpret_cast<f32x4*>(lds + kLdsBias)[i] = reinterpret_cast<const f32x4*>(packed + kOffBias)[i];
+  if (threadIdx.x < kNumFragMats) lds[kLdsScaleInv + threadIdx.x] = packed[kOffScale16 + kNumFragMats + threadIdx.x];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_sched_barrier(0);
+  const float* w0 = packed + s16_offset(0);
+  chunk_dma<8>(w0, lds, wave, lane);
+  chunk_dma<8>(w0 + 8 * 512, lds + kSlotFloats, wave, lane);
+  chunk_dma<8>(w0 + 2 * 8 * 512, lds + 2 * kSlotFloats, wave, lane);
   // PE in layout.h::pe_feature order (models.py:36-44): sin on lane half 0, cos on half 1.
   float pe[kPeSteps];
 #pragma unroll
@@ -181,29 +291,30 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     }
   pe[30] = h ? x[1] : x[0];
   pe[31] = h ? 0.0f : x[2];
+  float* pe_mine = lds + kLdsPe + wave * kPeSteps * 64;
 #pragma unroll
-  for (int p = 0; p < kPeSteps; ++p) pe_lds[wave][p][lane] = pe[p];
+  for (int p = 0; p < kPeSteps; ++p) pe_mine[p * 64 + lane] = pe[p];
   const float m_pe = fmaxf(1.0f, fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2]))));   // bounds |PE|
 
-  const float* scale_inv = packed + kOffScale16 + kNumFragMats;   // 1/s_w per matrix
-  const float* bias = packed + kOffBias;
+  const float* scale_inv = lds + kLdsScaleInv;                     // 1/s_w per matrix
+  const float* bias = lds + kLdsBias;
   float inv_s;
   float sc = pow2_scale(m_pe, inv_s);
   Operand pe_op[4];
   pe_operands(pe, sc, pe_op);
   float inv = inv_s * scale_inv[0];
 
-  f32x4 st[2][4];
-  const float* w0 = packed + s16_offset(0);
-  chunk_load<8>(st[0], w0, wave, lane);
-  chunk_load<8>(st[1], w0 + 8 * 512, wave, lane);
-  chunk_store<8>(st[0], ring[0], wave, lane);
-  __syncthreads();
+  wait_vmcnt<2 * 2 * 8 / kW16Waves>();     // this wave's part of chunk 0 landed (chunks 1-2 in flight)
+  __builtin_amdgcn_s_barrier();
+  h16x8 a0[4][2], a1[4][2];
+  read_half<8, 0>(lds, a0, lane);
 
   f32x16 acc[8];
   Operand in[16];
+  STAMP16(1);
   // layer 0: PE(63) -> 256
-  dense16<8, 0, 4, 8>(w0, packed + s16_offset(1), st, ring, in, pe_op, acc, wave, lane);
+  dense16<8, 0, 4, 8>(w0, packed + s16_offset(1), lds, a0, a1, in, pe_op, acc, wave, lane);
+  STAMP16(2);
   float m = unscale<8>(acc, inv, bias, h);
   // layers 1..7; layer 4 reads [h3, enc_x] (models.py:128-134), its PE re-split at h3's scale
 #pragma unroll 1
@@ -213,22 +324,24 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     to_operands(acc, sc, in);
     inv = inv_s * scale_inv[L];
     const float* wl = packed + s16_offset(L);
+    STAMP16(1 + 2 * L);
     if (L == kSkipLayer) {
       float pe2[kPeSteps];
 #pragma unroll
-      for (int p = 0; p < kPeSteps; ++p) pe2[p] = pe_lds[wave][p][lane];
+      for (int p = 0; p < kPeSteps; ++p) pe2[p] = pe_mine[p * 64 + lane];
       pe_operands(pe2, sc, pe_op);
-      dense16<8, 16, 4, 8>(wl, packed + s16_offset(L + 1), st, ring, in, pe_op, acc, wave, lane);
+      dense16<8, 16, 4, 8>(wl, packed + s16_offset(L + 1), lds, a0, a1, in, pe_op, acc, wave, lane);
     } else if (L == 7) {
-      dense16<8, 16, 0, 4>(wl, packed + s16_offset(8), st, ring, in, pe_op, acc, wave, lane);
+      dense16<8, 16, 0, 4>(wl, packed + s16_offset(8), lds, a0, a1, in, pe_op, acc, wave, lane);
     } else {
-      dense16<8, 16, 0, 8>(wl, packed + s16_offset(L + 1), st, ring, in, pe_op, acc, wave, lane);
+      dense16<8, 16, 0, 8>(wl, packed + s16_offset(L + 1), lds, a0, a1, in, pe_op, acc, wave, lane);
     }
+    STAMP16(2 + 2 * L);
     m = unscale<8>(acc, inv, bias + L * kHidden, h);
   }
 
   // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
-  const float* ws = packed + kOffSigmaW;
+  const float* ws = lds + kLdsSigmaW;
   float part = 0.0f;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
@@ -238,14 +351,16 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
       for (int e = 0; e < 4; ++e) part = fmaf(w[e], fmaxf(acc[t][4 * q + e], 0.0f), part);
     }
-  const float sig = fmaxf(part + __shfl_xor(part, 32) + packed[kOffSigmaB], 0.0f);
+  const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
 
   // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
   // (models.py:141-156); the bracket and the appearance part come per ray in `feat`.
   sc = pow2_scale(m, inv_s);
   to_operands(acc, sc, in);
   inv = inv_s * scale_inv[8];
-  dense16<4, 16, 0, 0>(packed + s16_offset(8), nullptr, st, ring, in, pe_op, acc, wave, lane);
+  STAMP16(17);
+  dense16<4, 16, 0, 0>(packed + s16_offset(8), nullptr, lds, a0, a1, in, pe_op, acc, wave, lane);
+  STAMP16(18);
   const float* fr = feat + r * kRayFeat;
   const float* wr = packed + kOffRgbW;
   float pr[3] = {0.0f, 0.0f, 0.0f};
@@ -277,6 +392,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
   }
+  STAMP16(19);
 }
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
