@@ -61,28 +61,54 @@ NERF_HD inline float pack_value(const float* const* P, size_t e) {
   return (e - kOffRgbB < 3) ? P[P_RGB_B][e - kOffRgbB] : 0.0f;
 }
 
-// Number of (row, source column) pairs of fragment matrix m, and the i-th of them.
-NERF_HD inline int frag_src_cols(int m) { return frag_is_pe(m) ? kPosEnc : kHidden; }
-NERF_HD inline float frag_weight_at(const float* const* P, int m, int i) {
-  const int K = frag_src_cols(m);
-  return frag_weight(P, m, i / K, (m == kSkipPeMat ? kHidden : 0) + i % K);
+// ---- split-f16 stream (layout.h) -----------------------------------------------------------
+// Layer L's weight matrix in natural (row, column) order: rows 256 (128 for the colour layer),
+// columns 63 (layer 0), 319 (layer 4: [h, enc_x]), 256 otherwise (colour layer: its h part).
+NERF_HD inline int layer_rows(int L) { return L == 8 ? kDirHidden : kHidden; }
+NERF_HD inline int layer_cols(int L) { return L == 0 ? kPosEnc : (L == kSkipLayer ? kHidden + kPosEnc : kHidden); }
+NERF_HD inline float layer_weight(const float* const* P, int L, int row, int col) {
+  if (L == 8) return P[P_DIR_W][(size_t)row * (kHidden + kDirEnc) + col];
+  return P[2 * L][(size_t)row * layer_cols(L) + col];
 }
 
-// f16x3 word w (two halves) of the split region, given every matrix's scale s_w.
-NERF_HD inline uint32_t pack16_word(const float* const* P, const float* scale, size_t w) {
-  int i = 0;
-  size_t base = kOff16;
-  while (w + kOff16 >= base + s16_floats(s16_order(i))) base += s16_floats(s16_order(i++));
-  const int m = s16_order(i);
-  const size_t rel = w + kOff16 - base;
-  const int NT = frag_ntiles(m);
-  const int ks = (int)(rel / ((size_t)NT * 512));
-  const int r2 = (int)(rel % ((size_t)NT * 512));
-  const int t = r2 / 512, part = (r2 % 512) / 256, lane = (r2 % 256) / 4, jj = r2 % 4;
+// Row statistics of layer L: max |W|, max_row sum |W| (R), max |b| (B).
+NERF_HD inline void layer_row_stats(const float* const* P, int L, int row, float& mx, float& l1, float& bmax) {
+  mx = 0.0f;
+  l1 = 0.0f;
+  for (int c = 0; c < layer_cols(L); ++c) {
+    const float w = fabsf(layer_weight(P, L, row, c));
+    mx = fmaxf(mx, w);
+    l1 += w;
+  }
+  bmax = L < 8 ? fabsf(P[2 * L + 1][row]) : 0.0f;
+}
+
+NERF_HD inline void store_layer_consts(float* consts, int L, float mx, float l1, float bmax) {
+  const int e = s16_exponent(mx);
+  consts[kS16Sw + L] = ldexpf(1.0f, 14 - e);
+  consts[kS16InvW + L] = ldexpf(1.0f, e - 14);
+  if (L < 8) {
+    consts[kS16R + L] = l1 * 1.0001f;     // rounding margin on the float sum: the bound must hold
+    consts[kS16B + L] = bmax;
+  }
+}
+
+// f16x3 word w (two halves) of the stream, given the layer constants.
+NERF_HD inline uint32_t pack16_word(const float* const* P, const float* consts, size_t w) {
+  const int c = (int)(w / kChunkFloats), r = (int)(w % kChunkFloats);
+  int L = 0;
+  while (c >= s16_chunk0(L + 1)) ++L;
+  const int per_group = s16_layer_ks(L) / 2;
+  const int local = c - s16_chunk0(L), g = local / per_group, i = local % per_group;
+  const int piece = r / 256, lane = (r % 256) / 4, jj = r % 4;
+  const int kk = piece / 8, ti = (piece / 2) % 4, part = piece % 2;
+  const int ks = 2 * i + kk, t = 4 * g + ti;
+  const int m = s16_matrix(L, ks), ksm = s16_matrix_ks(L, ks);
   uint32_t word = 0;
   for (int k = 0; k < 2; ++k) {
     const int j = 2 * jj + k;
-    const float v = frag_weight(P, m, t * 32 + (lane & 31), s16_source_col(m, ks, lane >> 5, j)) * scale[m];
+    const float v =
+        frag_weight(P, m, t * 32 + (lane & 31), s16_source_col(m, ksm, lane >> 5, j)) * consts[kS16Sw + L];
     const _Float16 hi = (_Float16)v;
     const _Float16 out = part == 0 ? hi : (_Float16)(v - (float)hi);
     uint16_t bits;
@@ -99,24 +125,22 @@ __global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restric
   if (e < kOff16) packed[e] = e < kF32Floats ? pack_value(P.p, e) : 0.0f;
 }
 
-// One block per fragment matrix: s_w = 2^(14 - e) with max|W| < 2^e, and 1/s_w.
+// One block per layer: its scale, bound constants (layout.h).
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
-  const int m = blockIdx.x;
-  const int n = frag_ntiles(m) * 32 * frag_src_cols(m);
-  float mx = 0.0f;
-  for (int i = threadIdx.x; i < n; i += 256) mx = fmaxf(mx, fabsf(frag_weight_at(P.p, m, i)));
-  __shared__ float red[256];
-  red[threadIdx.x] = mx;
+  const int L = blockIdx.x;
+  float mx = 0.0f, l1 = 0.0f, bm = 0.0f;
+  if ((int)threadIdx.x < layer_rows(L)) layer_row_stats(P.p, L, threadIdx.x, mx, l1, bm);
+  __shared__ float red[3][256];
+  red[0][threadIdx.x] = mx;
+  red[1][threadIdx.x] = l1;
+  red[2][threadIdx.x] = bm;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+    if ((int)threadIdx.x < w)
+      for (int q = 0; q < 3; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const int e = s16_exponent(red[0]);
-    packed[kOffScale16 + m] = ldexpf(1.0f, 14 - e);
-    packed[kOffScale16 + kNumFragMats + m] = ldexpf(1.0f, e - 14);
-  }
+  if (threadIdx.x == 0) store_layer_consts(packed + kOffScale16, L, red[0][0], red[1][0], red[2][0]);
 }
 
 __global__ void __launch_bounds__(256) pack16_kernel(ParamPtrs P, float* __restrict__ packed) {
@@ -130,7 +154,9 @@ int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
   hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kOff16 + 255) / 256)), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("pack_kernel")) return rc;
-  hipLaunchKernelGGL(scale16_kernel, dim3(kNumFragMats), dim3(256), 0, s, P, packed);
+  if (hipMemsetAsync(packed + kOffScale16, 0, kS16Consts * sizeof(float), s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "pack: hipMemsetAsync failed");
+  hipLaunchKernelGGL(scale16_kernel, dim3(kS16Layers), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("scale16_kernel")) return rc;
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((kFragFloats + 255) / 256)), dim3(256), 0, s, P, packed);
   return check_launch("pack16_kernel");
@@ -138,18 +164,21 @@ int launch_pack(const float* const* params, float* packed, hipStream_t s) {
 
 static void pack_host(const float* const* P, float* packed) {
   for (size_t e = 0; e < kOff16; ++e) packed[e] = e < kF32Floats ? pack_value(P, e) : 0.0f;
-  float* scale = packed + kOffScale16;
-  for (int i = kOffScale16; i < (int)kPackedFloats; ++i) packed[i] = 0.0f;
-  for (int m = 0; m < kNumFragMats; ++m) {
-    const int n = frag_ntiles(m) * 32 * frag_src_cols(m);
-    float mx = 0.0f;
-    for (int i = 0; i < n; ++i) mx = fmaxf(mx, fabsf(frag_weight_at(P, m, i)));
-    const int e = s16_exponent(mx);
-    scale[m] = ldexpf(1.0f, 14 - e);
-    scale[kNumFragMats + m] = ldexpf(1.0f, e - 14);
+  float* consts = packed + kOffScale16;
+  for (int i = 0; i < kS16Consts; ++i) consts[i] = 0.0f;
+  for (int L = 0; L < kS16Layers; ++L) {
+    float mx = 0.0f, l1 = 0.0f, bm = 0.0f;
+    for (int row = 0; row < layer_rows(L); ++row) {
+      float a, b, c;
+      layer_row_stats(P, L, row, a, b, c);
+      mx = fmaxf(mx, a);
+      l1 = fmaxf(l1, b);
+      bm = fmaxf(bm, c);
+    }
+    store_layer_consts(consts, L, mx, l1, bm);
   }
   uint32_t* words = reinterpret_cast<uint32_t*>(packed);
-  for (size_t w = 0; w < kFragFloats; ++w) words[kOff16 + w] = pack16_word(P, scale, w);
+  for (size_t w = 0; w < kFragFloats; ++w) words[kOff16 + w] = pack16_word(P, consts, w);
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -70,29 +70,44 @@ constexpr size_t kF32Floats = kOffRgbB + 4;                     // end of the ex
 // ---- split-f16 ("f16x3") fragments: the same 10 matrices as f16 hi/lo pairs --------------------
 // The f16x3 MLP runs every dense layer on v_mfma_f32_32x32x16_f16 as three products
 // hi(W)hi(a) + hi(W)lo(a) + lo(W)hi(a), where x*s = hi + lo + O(2^-24 x*s) with hi = f16(x*s)
-// and lo = f16(x*s - hi), s a power of two (per matrix for W, per sample for a) that puts the
-// largest value just under 2^15.  The dropped lo*lo term is O(2^-24): fp32-level accuracy at
-// 3 x 32 MFMA cycles per 16-deep k-step against 8 x 64 for the exact f32 instruction.
+// and lo = f16(x*s - hi), s a power of two (per layer for W, per sample for a) that keeps every
+// value under 2^15.  The dropped lo*lo term is O(2^-24): fp32-level accuracy at 3 x 32 MFMA
+// cycles per 16-deep k-step against 8 x 64 for the exact f32 instruction.
 //
 // A k-step is 16 inputs; lane l supplies 8 of them, k = 8(l>>5) + j (j = 0..7), for row or
 // column l&31.  Activation k-step ks = 2t + s reads registers 8s..8s+7 of the previous layer's
 // accumulator tile t as they stand, so element j of lane half h is input feature
 // 32t + 16s + 8(j>>2) + 4h + (j&3).  PE k-step q reads PE slot p = 8q + j (pe_feature).
 //
-// The weights are stored in the order the kernel streams them: matrices in network order
-// (layer 0, 1, 2, 3, 4's activation part, 4's PE part, 5, 6, 7, dir_linear's h part), each as
-// k-step "chunks" of NT tiles x {hi, lo} "pieces" of 64 lanes x 8 halves (1 KiB).
-NERF_HD constexpr int s16_order(int i) { return i < 5 ? i : (i == 5 ? kSkipPeMat : i - 1); }
-NERF_HD constexpr int s16_ksteps(int m) { return frag_ksteps(m) / 8; }             // 16-deep k-steps
-NERF_HD constexpr size_t s16_floats(int m) { return (size_t)frag_ntiles(m) * s16_ksteps(m) * 512; }
-constexpr size_t kOff16 = (kF32Floats + 255) / 256 * 256;                  // 1 KiB aligned
-NERF_HD constexpr size_t s16_offset(int m) {
-  size_t off = kOff16;
-  for (int i = 0; s16_order(i) != m; ++i) off += s16_floats(s16_order(i));
-  return off;
+// Nine "layers" stream their weights in the order the kernel consumes them: trunk layers 0..7
+// (layer 4 = its activation part, matrix 4, then its PE part, matrix 9) and the colour layer
+// (dir_linear's h part, matrix 8).  A trunk layer's 8 output tiles run as two groups of 4
+// (tiles 0-3, then 4-7), each over all of the layer's k-steps; the colour layer is one group.
+// The stream is a sequence of 16 KiB CHUNKS, each 2 k-steps x 4 tiles x {hi, lo} "pieces" of
+// 64 lanes x 8 halves (1 KiB): piece (kk*4 + ti)*2 + part of chunk i of group g of layer L holds
+// k-step 2i + kk of tile 4g + ti.
+constexpr int kS16Layers = 9;                                    // 0..7 trunk, 8 = colour
+NERF_HD constexpr int s16_layer_ks(int L) { return L == 0 ? 4 : (L == kSkipLayer ? 20 : 16); }
+NERF_HD constexpr int s16_layer_groups(int L) { return L == 8 ? 1 : 2; }
+NERF_HD constexpr int s16_layer_chunks(int L) { return s16_layer_groups(L) * s16_layer_ks(L) / 2; }
+NERF_HD constexpr int s16_chunk0(int L) {                        // first chunk of layer L
+  int c = 0;
+  for (int i = 0; i < L; ++i) c += s16_layer_chunks(i);
+  return c;
 }
-constexpr size_t kOffScale16 = kOff16 + kFragFloats;          // s_w[10] then 1/s_w[10] (pad 32)
-constexpr size_t kPackedFloats = kOffScale16 + 32;
+constexpr int kS16Chunks = s16_chunk0(kS16Layers);               // 128
+constexpr int kChunkFloats = 4096;                               // 16 KiB
+static_assert(kS16Chunks * kChunkFloats == (int)kFragFloats, "the stream holds exactly the 10 matrices");
+constexpr size_t kOff16 = (kF32Floats + 255) / 256 * 256;       // 1 KiB aligned
+// Per-layer constants after the stream: s_w, 1/s_w (9 each); R = max row L1 norm of W over all of
+// the layer's inputs, B = max |bias| (8 trunk layers each); bound |y| <= R max|a| + B.
+constexpr size_t kOffScale16 = kOff16 + kFragFloats;
+constexpr int kS16Sw = 0, kS16InvW = 9, kS16R = 18, kS16B = 26, kS16Consts = 48;
+constexpr size_t kPackedFloats = kOffScale16 + kS16Consts;
+
+// Matrix and its k-step for k-step ks of layer L.
+NERF_HD inline int s16_matrix(int L, int ks) { return L == 8 ? 8 : (L == kSkipLayer && ks >= 16 ? kSkipPeMat : L); }
+NERF_HD inline int s16_matrix_ks(int L, int ks) { return L == kSkipLayer && ks >= 16 ? ks - 16 : ks; }
 
 // Index of a state_dict tensor in the 24-pointer parameter list of nerf_pack_weights.
 enum Param {

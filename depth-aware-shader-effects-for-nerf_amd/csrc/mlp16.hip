@@ -4,26 +4,34 @@
 // Arithmetic.  Every dense layer out^T = W . in^T runs on v_mfma_f32_32x32x16_f16 as
 //     hi(W) hi(a) + hi(W) lo(a) + lo(W) hi(a)       (f32 accumulation)
 // with x*s = hi + lo + O(2^-24 |x*s|), hi = f16(x*s), lo = f16(x*s - hi), and s a power of two:
-// per matrix for W (packed, layout.h) and per SAMPLE for the activations (each sample's largest
-// input maps just under 2^14).  A power-of-two scale of a column of B scales that column of the
-// product exactly, so the accumulator holds s_w * s_j * (W a) and one multiply by the exact
-// inverse recovers it.  The dropped lo*lo term and the split residual are both O(2^-24): the
-// result has fp32-level error (tests/test_gpu_parity.py measures it against float64 next to
-// the exact-f32 kernel in mlp.hip), at 3 x 32 MFMA cycles per 16-deep k-step instead of the
+// per layer for W (packed, layout.h) and per SAMPLE for the activations.  A power-of-two scale
+// of a column of B scales that column of the product exactly, so the accumulator holds
+// s_w * s_j * (W a) and one multiply by the exact inverse recovers it.  The dropped lo*lo term
+// and the split residual are both O(2^-24): the result has fp32-level error
+// (tests/test_gpu_parity.py::test_forward_accuracy_vs_float64 measures it against float64 next
+// to the exact-f32 kernel in mlp.hip), at 3 x 32 MFMA cycles per 16-deep k-step instead of the
 // f32 instruction's 8 x 64.
 //
-// Work decomposition.  One wave owns 32 samples and runs the whole network for them, as in
-// mlp.hip: a layer's 8 accumulator tiles are the next layer's B operands in place (layout.h,
-// "split-f16 fragments"), so activations never leave registers.  At 5.3x the f32 rate one wave
-// would need ~21 B/clk of weights from L2, so the 4 waves of a workgroup share the weight
-// stream: each 16-deep k-step ("chunk": NT tiles x {hi, lo} x 1 KiB) is loaded once per
-// workgroup, a quarter by each wave, one step ahead into registers, published into a 2-slot LDS
-// ring, and read back by all four waves with ds_read_b128 (one barrier per k-step).
+// Scales from a bound, not a max.  Layer L+1's inputs y_L are split at s = 2^(14-e) with
+// R_L max|a_L| + B_L < 2^e, where max|a_L| is the sample's largest input of layer L and R_L
+// (max row L1 norm of W_L) and B_L (max |bias|) are pack-time constants: |y_L| <= R_L max|a_L|
+// + B_L rigorously, so nothing overflows f16, and the scale is known before y_L exists.  (A
+// loose bound only moves the split's absolute error floor, 2^-25 of the scaled unit, further
+// below the sample's largest value.)  That lets outputs be converted tile by tile while MFMAs run:
 //
-// Epilogue of a layer (VALU): y = acc * (1/(s_w s_j)) + bias (the true pre-activation), the
-// per-sample max of ReLU(y) over the 256 neurons (both lane halves), the next scale s, and the
-// f16 hi/lo split of ReLU(y) * s into the next layer's operands.  The heads (sigma, rgb) run in
-// f32 on the unscaled activations, as in mlp.hip.
+// Schedule.  One wave owns 32 samples and runs the whole network for them; a layer's output
+// tiles are the next layer's B operands in place (layout.h), so activations never leave
+// registers.  A trunk layer's 8 tiles run as two groups of 4 over all k-steps.  The VALU
+// epilogue of group A's outputs (unscale + bias, ReLU, split into the next layer's operands
+// 0..7) runs in the MFMA shadow of group B's last 8 k-steps (operands 0..7 are dead by then);
+// group B's epilogue (operands 8..15) runs in the shadow of the next layer's group A first 8
+// k-steps, which read operands 0..7.  Only the prologue (PE) and the colour head stay exposed.
+//
+// Weight stream.  At 5.3x the f32 rate one wave would need ~21 B/clk of weights from L2, so the
+// 4 waves of a workgroup share the stream: each 16 KiB chunk (2 k-steps x 4 tiles x {hi, lo}) is
+// DMA'd once per workgroup (global_load_lds_dwordx4, a quarter by each wave) into a 4-slot LDS
+// ring three chunks ahead, published by a counted vmcnt wait + barrier, and read back by all
+// four waves with ds_read_b128 interleaved between the MFMAs.
 #include "common.h"
 
 namespace nerf {
@@ -33,7 +41,7 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 constexpr int kW16Waves = 4;           // waves per workgroup, one per SIMD; they share the weight stream
 
 #ifdef NERF_MLP16_STAMPS   // diagnostic build (scripts/microbench/mlp16_stamps.hip): per-wave segment clocks
-__device__ unsigned long long nerf16_stamps[65536][24];
+__device__ unsigned long long nerf16_stamps[65536][16];
 #define STAMP16(i)                                                                          \
   do {                                                                                      \
     __builtin_amdgcn_sched_barrier(0);                                                      \
@@ -55,12 +63,11 @@ __device__ __forceinline__ f32x16 mfma16(h16x8 a, h16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// Per-sample power-of-two scale for values bounded by m: s = 2^(14-e) with m < 2^e.
-__device__ __forceinline__ float pow2_scale(float m, float& inv) {
+// s = 2^(14-e) for a bound m < 2^e (frexp); m = 0 gives e = 0.
+__device__ __forceinline__ float pow2_scale(float m) {
   int e;
-  frexpf(m, &e);                       // m = f 2^e, f in [0.5, 1); m = 0 gives e = 0
+  frexpf(m, &e);
   e = e < -100 ? -100 : (e > 100 ? 100 : e);
-  inv = ldexpf(1.0f, e - 14);
   return ldexpf(1.0f, 14 - e);
 }
 
@@ -70,35 +77,47 @@ __device__ __forceinline__ void split_into(float x, Operand& op, int j) {
   op.lo[j] = (_Float16)(x - (float)h);
 }
 
-// ---- the shared weight stream ------------------------------------------------------------
-// LDS (one __shared__ array: a second object can make hipcc drain the DMA before every ds_read):
-//   [ring: 4 slots x 16 KiB][PE: 4 waves x 32 x 64 floats]
-//   [trunk biases 8 x 256 | density_head weight 256, bias 4 | 1/s_w of the 10 matrices, pad 16]
-// (every small vector the layers read sits in LDS: an ordinary global load used while a DMA is in
-// flight makes hipcc wait vmcnt(0), draining the stream)
-constexpr int kSlotFloats = 4096;
-constexpr int kLdsPe = 4 * kSlotFloats;
+// ---- LDS: one __shared__ array (a second object can make hipcc drain the DMA before every
+// ds_read).  [ring: 4 x 16 KiB][PE: 4 waves x 32 x 64][biases 8 x 256 | density_head w 256, b 4]
+// [layer constants].  Every small vector the layers read sits here: an ordinary global load used
+// while a DMA is in flight makes hipcc wait vmcnt(0), draining the stream.
+constexpr int kLdsPe = 4 * kChunkFloats;
 constexpr int kLdsBias = kLdsPe + kW16Waves * kPeSteps * 64;
 constexpr int kLdsSigmaW = kLdsBias + 8 * kHidden;
 constexpr int kLdsVecFloats = 8 * kHidden + kHidden + 4;    // kOffBias .. kOffSigmaB + 4, contiguous in `packed`
-constexpr int kLdsScaleInv = kLdsBias + kLdsVecFloats;
-constexpr int kLdsFloats = kLdsScaleInv + 16;               // 105 KiB
+constexpr int kLdsConsts = kLdsBias + kLdsVecFloats;
+constexpr int kLdsFloats = kLdsConsts + kS16Consts;          // 105 KiB
 static_assert(kOffSigmaW == kOffBias + 8 * kHidden && kOffSigmaB == kOffSigmaW + kHidden, "packed vector order");
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-// A chunk (one 16-deep k-step of NT tiles) is 2*NT pieces of 256 floats (64 lanes x 16 B); wave w
-// moves pieces w, w+4, ... straight into its LDS slot with global_load_lds_dwordx4 (no registers).
-template <int NT>
-__device__ __forceinline__ void chunk_dma(const float* __restrict__ chunk, float* slot, int wave, int lane) {
+// ---- the shared weight stream ------------------------------------------------------------
+// Chunk c (16 pieces of 1 KiB) into LDS slot SLOT; wave w moves pieces w, w+4, w+8, w+12.  Inline
+// asm in the saddr form (uniform 64-bit base in SGPRs + the lane's 32-bit offset `voff` =
+// 16*lane + 1024*wave, one VGPR for the whole kernel): the builtin's per-lane 64-bit addresses
+// cost 8 VGPRs per chunk.  hipcc counts none of these loads; the stream waits for them itself
+// (wait_vmcnt), and M0 is saved and restored around each.
+template <int SLOT>
+__device__ __forceinline__ void chunk_dma(const float* __restrict__ stream, int c, uint32_t lds_base, uint32_t voff) {
+  // lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece); voff: the
+  // lane's byte offset 16 * lane + 1024 * wave into the chunk
 #ifdef NERF16_T_NODMA
   return;
 #endif
+  const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
 #pragma unroll
-  for (int i = 0; i < 2 * NT / kW16Waves; ++i) {
-    const int p = wave + kW16Waves * i;
-    __builtin_amdgcn_global_load_lds((gptr_t)(chunk + p * 256 + lane * 4), (lptr_t)(slot + p * 256), 16, 0, 0);
+  for (int i = 0; i < 4; ++i) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(src + i * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + i * (kW16Waves * 1024))
+        : "memory");
   }
 }
 
@@ -106,142 +125,140 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }   // lgkmcnt(0) only
 
-// A fragments of half a chunk (tiles HALF*NT/2 ..), hi and lo per tile.
-template <int NT, int HALF>
-__device__ __forceinline__ void read_half(const float* slot, h16x8 (&a)[4][2], int lane) {
+// A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
+template <int KK>
+__device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
 #ifdef NERF16_T_NOREAD
 #pragma unroll
-  for (int i = 0; i < NT / 2; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
   return;
 #endif
 #pragma unroll
-  for (int i = 0; i < NT / 2; ++i) {
-    const int t = HALF * (NT / 2) + i;
-    a[i][0] = __builtin_bit_cast(h16x8, *reinterpret_cast<const f32x4*>(slot + (2 * t) * 256 + lane * 4));
-    a[i][1] = __builtin_bit_cast(h16x8, *reinterpret_cast<const f32x4*>(slot + (2 * t + 1) * 256 + lane * 4));
-  }
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+      a[ti][part] = __builtin_bit_cast(
+          h16x8, *reinterpret_cast<const f32x4*>(slot + ((KK * 4 + ti) * 2 + part) * 256 + lane * 4));
 }
 
-template <int NT, int HALF, bool FIRST>
-__device__ __forceinline__ void mfma_half(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8]) {
+// One k-step of group G (tiles 4G .. 4G+3).
+template <int G, bool FIRST>
+__device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8]) {
 #ifdef NERF16_T_NOMFMA   // timing-only builds (scripts/microbench/mlp16_stamps.hip); wrong results
 #pragma unroll
-  for (int i = 0; i < NT / 2; ++i)
-    asm volatile("" : "+v"(acc[HALF * (NT / 2) + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[4 * G + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
   return;
 #endif
-  static_for<NT / 2>([&](auto ic) __attribute__((always_inline)) {
+  static_for<4>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
-    constexpr int t = HALF * (NT / 2) + i;
     f32x16 c;
     if constexpr (FIRST) c = mfma16(a[i][1], b.hi, f32x16{});
-    else c = mfma16(a[i][1], b.hi, acc[t]);
+    else c = mfma16(a[i][1], b.hi, acc[4 * G + i]);
     c = mfma16(a[i][0], b.lo, c);
-    acc[t] = mfma16(a[i][0], b.hi, c);
+    acc[4 * G + i] = mfma16(a[i][0], b.hi, c);
   });
 }
 
-// DMA instructions one wave issues for chunk j of a layer with KS chunks of NT tiles followed by
-// a matrix of NEXT_NT tiles (0: the stream ends).
-template <int NT, int KS, int NEXT_NT>
-__device__ __forceinline__ constexpr int dma_per_wave(int j) {
-  return j < KS ? 2 * NT / kW16Waves : 2 * NEXT_NT / kW16Waves;
-}
-
-// Half a k-step: the MFMAs of tiles HALF*NT/2 .. from the fragments in `am`, interleaved with
-// the reads of the next half's fragments into `ar` (RT tiles' worth, from `slot_r`; 0 = none):
-// 2 ds_read_b128 between consecutive tiles' 3 MFMAs, so the LDS latency hides under them.
-template <int NT, int HALF, bool FIRST, int RT, int RHALF>
+// Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
+// (into `ar`, from `slot_r`) and the side work (VALU) interleaved: 2 ds_read_b128 between
+// consecutive tiles' 3 MFMAs; the VALU fills the MFMA shadow.
+template <int G, bool FIRST, bool READ, int KK_R, typename Side>
 __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
-                                          const float* slot_r, h16x8 (&ar)[4][2], int lane) {
-  if constexpr (RT > 0) read_half<RT, RHALF>(slot_r, ar, lane);
-  mfma_half<NT, HALF, FIRST>(am, b, acc);
-  static_for<NT / 2>([&](auto ic) __attribute__((always_inline)) {
-    constexpr int i = decltype(ic)::value;
-    if constexpr (i < RT / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
-    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                            // 3 MFMAs
-  });
+                                          const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side) {
+  if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
+  mfma_kstep<G, FIRST>(am, b, acc);
+  side();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (READ) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                      // 3 MFMAs
+  }
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One dense layer: NT output tiles, KS_ACT activation k-steps from `in` then KS_PE PE k-steps
-// from `pe`, weights at `wm` (stream order; layer 4's PE part follows its activation part).
-// Pipeline per k-step ks (chunk ks sits in LDS slot ks&3):
-//   MFMA half 0, reading half 1's A | wait own DMA of chunk ks+1, barrier | DMA chunk ks+3 into
-//   the slot chunk ks-1 used | MFMA half 1, reading chunk ks+1's half-0 A
-// On entry chunk 0 is published, chunks 1-2 are in flight and a0 holds chunk 0's half 0; on exit
-// the same holds for `next` (NEXT_NT tiles; 0 = last matrix).
-template <int NT, int KS_ACT, int KS_PE, int NEXT_NT>
-__device__ __forceinline__ void dense16(const float* __restrict__ wm, const float* __restrict__ next, float* lds,
-                                        h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand (&in)[16],
-                                        const Operand (&pe)[4], f32x16 (&acc)[8], int wave, int lane) {
-  constexpr int KS = KS_ACT + KS_PE;
-  static_assert(KS % 4 == 0, "every matrix starts on LDS slot 0");
-  static_for<KS>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int ks = decltype(kc)::value;
-    const Operand& b = [&]() -> const Operand& {
-      if constexpr (ks < KS_ACT) return in[ks];
-      else return pe[ks - KS_ACT];
-    }();
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): a0's reads (interleaved in the last half-step) are in
-    half_step<NT, 0, ks == 0, NT, 1>(a0, b, acc, lds + (ks & 3) * kSlotFloats, a1, lane);
-    constexpr bool has1 = ks + 1 < KS || NEXT_NT > 0;
-    constexpr bool has2 = ks + 2 < KS || NEXT_NT > 0;
-    constexpr bool has3 = ks + 3 < KS || NEXT_NT > 0;
+// Chunk-step: k-steps 2i, 2i+1 of group G from the chunk in LDS slot SLOT (global chunk c);
+// FIRST (the group's first chunk) starts the accumulators from 0 at k-step 0.
+//   MFMA k-step 0, reading k-step 1's A | wait own DMA of chunk c+1, barrier | DMA chunk c+3 into
+//   the slot chunk c-1 used | MFMA k-step 1, reading chunk c+1's k-step-0 A
+// On entry chunk c is published, c+1 and c+2 are in flight and a0 holds k-step 0's fragments.
+// TAIL = chunks left after c, capped at 3: the stream's last steps stop loading and waiting.
+template <int G, int SLOT, bool FIRST, int TAIL, typename Side0, typename Side1>
+__device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int c, float* lds, uint32_t lds_dma,
+                                           uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
+                                           const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
+                                           Side1&& side1) {
+  wait_lgkm0();                                     // a0's reads (interleaved in the last half-step) are in
+  half_step<G, FIRST, true, 1>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0);
 #ifndef NERF16_T_NOBARRIER
-    if constexpr (has1) {
-      wait_vmcnt<has2 ? dma_per_wave<NT, KS, NEXT_NT>(ks + 2) : 0>();
-      __builtin_amdgcn_s_barrier();
-    }
+  if constexpr (TAIL >= 1) {
+    wait_vmcnt<TAIL >= 2 ? 4 : 0>();
+    __builtin_amdgcn_s_barrier();
+  }
 #endif
-    if constexpr (ks + 3 < KS) chunk_dma<NT>(wm + (size_t)(ks + 3) * NT * 512, lds + ((ks + 3) & 3) * kSlotFloats, wave, lane);
-    else if constexpr (has3)
-      chunk_dma<NEXT_NT>(next + (size_t)(ks + 3 - KS) * NEXT_NT * 512, lds + ((ks + 3) & 3) * kSlotFloats, wave, lane);
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // a1's reads are in
-    constexpr int RT = ks + 1 < KS ? NT : NEXT_NT;
-    half_step<NT, 1, ks == 0, RT, 0>(a1, b, acc, lds + ((ks + 1) & 3) * kSlotFloats, a0, lane);
+  if constexpr (TAIL >= 3) chunk_dma<(SLOT + 3) & 3>(stream, c + 3, lds_dma, voff);
+  wait_lgkm0();                                     // a1's reads are in
+  half_step<G, false, (TAIL >= 1), 0>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0, lane, side1);
+}
+
+// A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
+// the B operand of k-step 2i+kk; side(i, kk) is the VALU work placed in that half-step.
+// TAIL_END = chunks after this group (capped at 3).
+template <int G, int NSTEP, int SLOT0, int TAIL_END, typename Opnd, typename Side>
+__device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
+                                          uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], f32x16 (&acc)[8],
+                                          int lane, Opnd&& operand, Side&& side) {
+  static_for<NSTEP>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    constexpr int left = NSTEP - 1 - i + TAIL_END;
+    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3)>(
+        stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
+        operand(ic, std::integral_constant<int, 1>{}), acc, lane,
+        [&]() __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}); },
+        [&]() __attribute__((always_inline)) { side(ic, std::integral_constant<int, 1>{}); });
   });
 }
 
-// acc[t] <- y = acc * inv + vec[neuron] for the NT tiles (vec: biases, or a per-ray row);
-// returns the sample's max of ReLU(y) (lane halves combined).
-template <int NT>
-__device__ __forceinline__ float unscale(f32x16 (&acc)[8], float inv, const float* __restrict__ vec, int h) {
-  float m = 0.0f;
-  static_for<NT>([&](auto tc) __attribute__((always_inline)) {
-    constexpr int t = decltype(tc)::value;
+// ---- epilogue pieces (the side work) ----------------------------------------------------------
+// Registers 8SH..8SH+7 of output tile T -> the next layer's operand `op`:
+//   y = acc*inv + bias, r = ReLU(y), op = split(r*s); m tracks max r; SIGMA adds ws . r to part.
+template <int T, int SH, bool SIGMA>
+__device__ __forceinline__ void convert8(const f32x16 (&acc)[8], float inv, const float* bias, float s, Operand& op,
+                                         float& m, float& part, const float* ws, int h) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(vec + t * 32 + 8 * q + 4 * h);
+  for (int qq = 0; qq < 2; ++qq) {
+    const int q = 2 * SH + qq;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
+    f32x4 w;
+    if constexpr (SIGMA) w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y = fmaf(acc[t][4 * q + e], inv, b[e]);
-        acc[t][4 * q + e] = y;
-        m = fmaxf(m, y);
-      }
+    for (int e = 0; e < 4; ++e) {
+      const float r = fmaxf(fmaf(acc[T][8 * SH + 4 * qq + e], inv, b[e]), 0.0f);
+      m = fmaxf(m, r);
+      if constexpr (SIGMA) part = fmaf(w[e], r, part);
+      split_into(r * s, op, 4 * qq + e);
     }
-  });
-  return fmaxf(m, __shfl_xor(m, 32));
+  }
 }
 
-// The next layer's operands: split(ReLU(acc) * s) in the k-step order of layout.h.
-__device__ __forceinline__ void to_operands(const f32x16 (&acc)[8], float s, Operand (&in)[16]) {
-  static_for<8>([&](auto tc) __attribute__((always_inline)) {
-    constexpr int t = decltype(tc)::value;
+// PE operand Q split at scale s from this wave's LDS copy (layer 4 reads [h3, enc_x]).
+template <int Q>
+__device__ __forceinline__ void pe_operand(const float* pe_mine, float s, Operand& op, int lane) {
 #pragma unroll
-    for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) split_into(fmaxf(acc[t][8 * sh + j], 0.0f) * s, in[2 * t + sh], j);
-  });
+  for (int j = 0; j < 8; ++j) split_into(pe_mine[(8 * Q + j) * 64 + lane] * s, op, j);
 }
 
-__device__ __forceinline__ void pe_operands(const float (&pe)[kPeSteps], float s, Operand (&op)[4]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) split_into(pe[8 * q + j] * s, op[q], j);
-}
+// The sample's max over both lane halves.
+__device__ __forceinline__ float sample_max(float m) { return fmaxf(m, __shfl_xor(m, 32)); }
+
+struct NoSide {
+  template <typename A, typename B>
+  __device__ __forceinline__ void operator()(A, B) const {}
+};
+
+template <typename I, typename K>
+__device__ __forceinline__ constexpr int kstep_of(I, K) { return 2 * I::value + K::value; }
 
 __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
@@ -249,7 +266,6 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
              float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
   __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
-
   STAMP16(0);
   const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
   // every wave runs to the end (the weight stream has barriers); tail lanes repeat sample M-1
@@ -267,18 +283,20 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
     for (int c = 0; c < 3; ++c) x[c] = orig[3 * s + c];
   }
-  // small vectors into LDS, then the weight stream starts: chunks 0-2 of layer 0 in flight while
-  // the PE is computed (every ordinary load retired first: hipcc waits vmcnt(0) at the use of an
-  // ordinary load while a DMA is in flight)
+  // Small vectors into LDS, then the weight stream starts: chunks 0-2 in flight while the PE is
+  // computed (every ordinary load retired first, see the LDS note).
   for (int i = threadIdx.x; i < kLdsVecFloats / 4; i += 64 * kW16Waves)
     reinterpret_cast<f32x4*>(lds + kLdsBias)[i] = reinterpret_cast<const f32x4*>(packed + kOffBias)[i];
-  if (threadIdx.x < kNumFragMats) lds[kLdsScaleInv + threadIdx.x] = packed[kOffScale16 + kNumFragMats + threadIdx.x];
+  if (threadIdx.x < kS16Consts) lds[kLdsConsts + threadIdx.x] = packed[kOffScale16 + threadIdx.x];
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_sched_barrier(0);
-  const float* w0 = packed + s16_offset(0);
-  chunk_dma<8>(w0, lds, wave, lane);
-  chunk_dma<8>(w0 + 8 * 512, lds + kSlotFloats, wave, lane);
-  chunk_dma<8>(w0 + 2 * 8 * 512, lds + 2 * kSlotFloats, wave, lane);
+  const float* stream = packed + kOff16;
+  const uint32_t lds_dma = (uint32_t)(uintptr_t)(lptr_t)lds + 1024u * wave;   // this wave's first piece
+  const uint32_t voff = 16u * lane + 1024u * wave;
+  chunk_dma<0>(stream, 0, lds_dma, voff);
+  chunk_dma<1>(stream, 1, lds_dma, voff);
+  chunk_dma<2>(stream, 2, lds_dma, voff);
+
   // PE in layout.h::pe_feature order (models.py:36-44): sin on lane half 0, cos on half 1.
   float pe[kPeSteps];
 #pragma unroll
@@ -296,71 +314,132 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   for (int p = 0; p < kPeSteps; ++p) pe_mine[p * 64 + lane] = pe[p];
   const float m_pe = fmaxf(1.0f, fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2]))));   // bounds |PE|
 
-  const float* scale_inv = lds + kLdsScaleInv;                     // 1/s_w per matrix
   const float* bias = lds + kLdsBias;
-  float inv_s;
-  float sc = pow2_scale(m_pe, inv_s);
+  const float* ws = lds + kLdsSigmaW;
+  const float* cst = lds + kLdsConsts;
+  // s_cur: scale of the current layer's inputs; inv_cur unscales its accumulators; s_nxt: scale
+  // of the next layer's inputs (from the bound on this layer's outputs).
+  float s_cur = pow2_scale(m_pe);
   Operand pe_op[4];
-  pe_operands(pe, sc, pe_op);
-  float inv = inv_s * scale_inv[0];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split_into(pe[8 * q + j] * s_cur, pe_op[q], j);
 
-  wait_vmcnt<2 * 2 * 8 / kW16Waves>();     // this wave's part of chunk 0 landed (chunks 1-2 in flight)
+  wait_vmcnt<8>();                                          // this wave's part of chunk 0 (chunks 1-2 in flight)
   __builtin_amdgcn_s_barrier();
   h16x8 a0[4][2], a1[4][2];
-  read_half<8, 0>(lds, a0, lane);
+  read_kstep<0>(lds, a0, lane);
 
   f32x16 acc[8];
   Operand in[16];
+  float m = 0.0f, part = 0.0f;
+  float inv_cur = cst[kS16InvW + 0] / s_cur;                // exact: powers of two
+  float s_nxt = pow2_scale(cst[kS16R + 0] * m_pe + cst[kS16B + 0]);
   STAMP16(1);
-  // layer 0: PE(63) -> 256
-  dense16<8, 0, 4, 8>(w0, packed + s16_offset(1), lds, a0, a1, in, pe_op, acc, wave, lane);
+
+  // ---- layer 0: PE(63) -> 256, 2 chunk-steps per group ----
+  auto pe_operand_of = [&](auto i, auto kk) -> const Operand& { return pe_op[kstep_of(i, kk)]; };
+  run_group<0, 2, 0, 3>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
+  // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE)
+  run_group<1, 2, 2, 3>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
+                        [&](auto i, auto kk) __attribute__((always_inline)) {
+                          constexpr int t = kstep_of(i, kk);   // tiles 0..3
+                          convert8<t, 0, false>(acc, inv_cur, bias, s_nxt, in[2 * t], m, part, ws, h);
+                          convert8<t, 1, false>(acc, inv_cur, bias, s_nxt, in[2 * t + 1], m, part, ws, h);
+                        });
   STAMP16(2);
-  float m = unscale<8>(acc, inv, bias, h);
-  // layers 1..7; layer 4 reads [h3, enc_x] (models.py:128-134), its PE re-split at h3's scale
+
+  // ---- layers 1..7 ----
+  // On entry to layer L: operands 0..7 hold y_{L-1} tiles 0-3 split at s_cur, y_{L-1} tiles 4-7
+  // wait in acc[4..7], m holds the max of ReLU(y_{L-1}) tiles 0-3.
+  //
+  // Side-work schedule, by half-step hs = 2*(chunk-step) + k-step-in-chunk (one half-tile
+  // conversion every other half-step, so the VALU stays inside the MFMA shadow):
+  //  * group A converts y_{L-1} tile 4+i half sh into operand 8+2i+sh at hs = 4i + 2sh; that
+  //    operand is first read at hs = 8+2i+sh, and acc[4..7] is free again before group B;
+  //  * group B converts y_L tile t half sh into operand 2t+sh at hs = 4t + 2sh + 1; that operand
+  //    was last read at hs = 2t+sh, and is next read at the next layer's hs = 2t+sh.
+  float inv_prev = inv_cur;
+  const float* bias_prev = bias;
+  s_cur = s_nxt;
+  auto act_operand = [&](auto i, auto kk) -> const Operand& { return in[kstep_of(i, kk)]; };
+  auto op4 = [&](auto i, auto kk) -> const Operand& {
+    constexpr int ks = kstep_of(i, kk);
+    if constexpr (ks < 16) return in[ks];
+    else return pe_op[ks - 16];
+  };
+  // group A's side: y_{L-1} tiles 4-7 (SIGMA: also the density head's dot product)
+  auto side_prev = [&](auto i, auto kk, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk);
+    if constexpr (hs % 2 == 0 && hs < 16) {
+      constexpr int t = 4 + hs / 4, sh = (hs / 2) % 2;
+      convert8<t, sh, decltype(sigma_tag)::value>(acc, inv_prev, bias_prev, s_cur, in[2 * t + sh], m, part, ws, h);
+    }
+  };
+  // group B's side: this layer's y_L tiles 0-3
+  auto side_cur = [&](auto i, auto kk, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk);
+    if constexpr (hs % 2 == 1 && hs < 16) {
+      constexpr int t = hs / 4, sh = (hs / 2) % 2;
+      convert8<t, sh, decltype(sigma_tag)::value>(acc, inv_cur, bias_l, s_nxt, in[2 * t + sh], m, part, ws, h);
+    }
+  };
+  using NoSigma = std::false_type;
+  using Sigma = std::true_type;
 #pragma unroll 1
   for (int L = 1; L < 8; ++L) {
-    if (L == kSkipLayer) m = fmaxf(m, m_pe);
-    sc = pow2_scale(m, inv_s);
-    to_operands(acc, sc, in);
-    inv = inv_s * scale_inv[L];
-    const float* wl = packed + s16_offset(L);
-    STAMP16(1 + 2 * L);
+    inv_cur = cst[kS16InvW + L] / s_cur;
+    const float* bias_l = bias + L * kHidden;
+    const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
+    // group A (k-steps 0..15, + PE 16..19 at layer 4)
     if (L == kSkipLayer) {
-      float pe2[kPeSteps];
-#pragma unroll
-      for (int p = 0; p < kPeSteps; ++p) pe2[p] = pe_mine[p * 64 + lane];
-      pe_operands(pe2, sc, pe_op);
-      dense16<8, 16, 4, 8>(wl, packed + s16_offset(L + 1), lds, a0, a1, in, pe_op, acc, wave, lane);
-    } else if (L == 7) {
-      dense16<8, 16, 0, 4>(wl, packed + s16_offset(8), lds, a0, a1, in, pe_op, acc, wave, lane);
+      // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur in the free odd half-steps
+      // 1, 3, 5, 7 (read from hs 16)
+      run_group<0, 10, 0, 3>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+                             [&](auto i, auto kk) __attribute__((always_inline)) {
+                               constexpr int hs = kstep_of(i, kk);
+                               side_prev(i, kk, NoSigma{});
+                               if constexpr (hs % 2 == 1 && hs < 8) pe_operand<hs / 2>(pe_mine, s_cur, pe_op[hs / 2], lane);
+                             });
     } else {
-      dense16<8, 16, 0, 8>(wl, packed + s16_offset(L + 1), lds, a0, a1, in, pe_op, acc, wave, lane);
+      run_group<0, 8, 0, 3>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, NoSigma{}); });
     }
-    STAMP16(2 + 2 * L);
-    m = unscale<8>(acc, inv, bias + L * kHidden, h);
+    // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
+    m = sample_max(m);
+    float bound = cst[kS16R + L] * (L == kSkipLayer ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
+    if (L + 1 == kSkipLayer) bound = fmaxf(bound, m_pe);    // layer 4 splits the PE at the same scale
+    s_nxt = pow2_scale(bound);
+    m = 0.0f;
+    // group B (layer 7 also starts the density head)
+    if (L == kSkipLayer) {
+      run_group<1, 10, 2, 3>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+                             [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
+    } else if (L == 7) {
+      run_group<1, 8, 0, 3>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, Sigma{}); });
+    } else {
+      run_group<1, 8, 0, 3>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
+    }
+    inv_prev = inv_cur;
+    bias_prev = bias_l;
+    s_cur = s_nxt;
+    STAMP16(2 + L);
   }
 
-  // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
-  const float* ws = lds + kLdsSigmaW;
-  float part = 0.0f;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(ws + t * 32 + 8 * q + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) part = fmaf(w[e], fmaxf(acc[t][4 * q + e], 0.0f), part);
-    }
-  const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
+  // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
+  // operands 8..15 and finishes the density head ----
+  inv_cur = cst[kS16InvW + 8] / s_cur;
+  run_group<0, 8, 0, 0>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                        [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, Sigma{}); });
+  STAMP16(10);
 
+  // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
+  const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
   // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
   // (models.py:141-156); the bracket and the appearance part come per ray in `feat`.
-  sc = pow2_scale(m, inv_s);
-  to_operands(acc, sc, in);
-  inv = inv_s * scale_inv[8];
-  STAMP16(17);
-  dense16<4, 16, 0, 0>(packed + s16_offset(8), nullptr, lds, a0, a1, in, pe_op, acc, wave, lane);
-  STAMP16(18);
   const float* fr = feat + r * kRayFeat;
   const float* wr = packed + kOffRgbW;
   float pr[3] = {0.0f, 0.0f, 0.0f};
@@ -372,7 +451,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
       const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
       float hd[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv, fd[e]), 0.0f) + ap[e];
+      for (int e = 0; e < 4; ++e) hd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f) + ap[e];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
@@ -392,7 +471,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
   }
-  STAMP16(19);
+  STAMP16(11);
 }
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,

@@ -2,8 +2,8 @@
 // coarse pass of an 800x800 frame (640,000 rays x 64 samples), synthetic inputs.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNERF_MLP16_STAMPS \
 //     -I depth-aware-shader-effects-for-nerf_amd/csrc -o scripts/microbench/mlp16_stamps scripts/microbench/mlp16_stamps.hip
-// Stamps: 0 start | 1 prologue done (PE, first chunk) | per layer L: 1+2L before its k-loop, 2+2L
-// after it (the epilogue runs between 2+2L and 3+2L) | 17/18 around the colour layer | 19 end.
+// Stamps: 0 start | 1 prologue done (PE, first chunk) | 2 + L after trunk layer L (0..7; each
+// layer's epilogue runs inside the next layer's MFMAs) | 10 after the colour layer | 11 end.
 #include "../../depth-aware-shader-effects-for-nerf_amd/csrc/mlp16.hip"
 #include <algorithm>
 #include <stdarg.h>
@@ -16,7 +16,11 @@ int main() {
   std::vector<float> h(nerf::kPackedFloats);
   srand(1);
   for (auto& v : h) v = ((float)rand() / RAND_MAX - 0.5f) * 0.1f;
-  for (int m = 0; m < nerf::kNumFragMats; ++m) { h[nerf::kOffScale16 + m] = 65536.f; h[nerf::kOffScale16 + 10 + m] = 1.f / 65536.f; }
+  for (int L = 0; L < nerf::kS16Layers; ++L) {
+    h[nerf::kOffScale16 + nerf::kS16Sw + L] = 65536.f;
+    h[nerf::kOffScale16 + nerf::kS16InvW + L] = 1.f / 65536.f;
+    if (L < 8) { h[nerf::kOffScale16 + nerf::kS16R + L] = 8.f; h[nerf::kOffScale16 + nerf::kS16B + L] = 0.1f; }
+  }
   float *packed, *o, *d, *z, *feat, *rgb, *sig;
   (void)hipMalloc(&packed, h.size() * 4);
   (void)hipMemcpy(packed, h.data(), h.size() * 4, hipMemcpyHostToDevice);
@@ -40,19 +44,11 @@ int main() {
   (void)hipDeviceSynchronize();
   float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
-  static unsigned long long st[65536][24];
+  static unsigned long long st[65536][16];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(nerf::nerf16_stamps), sizeof(st));
   struct Seg { const char* name; int a, b; };
-  std::vector<Seg> segs = {{"prologue", 0, 1}};
-  static char names[40][16];
-  int k = 0;
-  for (int L = 0; L < 8; ++L) {
-    snprintf(names[k], 16, "L%d k-loop", L); segs.push_back({names[k++], 1 + 2 * L, 2 + 2 * L});
-    snprintf(names[k], 16, "L%d epilogue", L); segs.push_back({names[k++], 2 + 2 * L, 3 + 2 * L});
-  }
-  segs.back().b = 17;   // L7's epilogue runs into the colour layer's operand split
-  segs.push_back({"dir k-loop", 17, 18});
-  segs.push_back({"heads", 18, 19});
+  std::vector<Seg> segs = {{"prologue", 0, 1}, {"L0", 1, 2}, {"L1", 2, 3}, {"L2", 3, 4}, {"L3", 4, 5}, {"L4", 5, 6},
+                           {"L5", 6, 7}, {"L6", 7, 8}, {"L7", 8, 9}, {"colour", 9, 10}, {"heads", 10, 11}};
   double sum = 0;
   for (auto& sg : segs) {
     std::vector<double> v;
@@ -62,7 +58,7 @@ int main() {
     sum += v[v.size() / 2];
   }
   std::vector<double> tot;
-  for (int w = 0; w < 65536; ++w) tot.push_back((double)(st[w][19] - st[w][0]));
+  for (int w = 0; w < 65536; ++w) tot.push_back((double)(st[w][11] - st[w][0]));
   std::sort(tot.begin(), tot.end());
   printf("total median %.0f (sum of medians %.0f) memtime ticks; MFMA floor 98304 cycles per wave; kernel %.2f ms\n",
          tot[tot.size() / 2], sum, ms);

@@ -173,19 +173,27 @@ def test_emulated_kernel_matches_oracle(ref_state, app_vec):
 
 
 # ---- the split-f16 ("f16x3") region of the packed buffer (layout.h, csrc/mlp16.hip)
-S16_ORDER = (0, 1, 2, 3, 4, 9, 5, 6, 7, 8)
+def s16_layer_ks(L):
+    return 4 if L == 0 else (20 if L == 4 else 16)
 
 
-def s16_ksteps(m):
-    return frag_ksteps(m) // 8
+def s16_layer_groups(L):
+    return 1 if L == 8 else 2
 
 
-def s16_offset(m):
-    off = (frag_offset(10) + 8 * 256 + 256 + 4 + 128 + 128 * 27 + 128 * 32 + 128 + 384 + 4 + 255) // 256 * 256
-    for i in S16_ORDER:
-        if i == m:
-            return off
-        off += frag_ntiles(i) * s16_ksteps(i) * 512
+def s16_chunk0(L):
+    return sum(s16_layer_groups(i) * s16_layer_ks(i) // 2 for i in range(L))
+
+
+def s16_base():
+    f32_floats = frag_offset(10) + 8 * 256 + 256 + 4 + 128 + 128 * 27 + 128 * 32 + 128 + 384 + 4
+    return (f32_floats + 255) // 256 * 256
+
+
+def s16_consts(packed):
+    base = s16_base() + frag_offset(10)
+    c = packed[base: base + 48].astype(np.float64)
+    return {"s_w": c[0:9], "inv_w": c[9:18], "R": c[18:26], "B": c[26:34]}
 
 
 def s16_source_col(m, ks, h, j):
@@ -196,48 +204,55 @@ def s16_source_col(m, ks, h, j):
     return f if f < 0 else (256 if m == 9 else 0) + f
 
 
-def s16_matrix(packed, m):
-    """(hi, lo, s_w) of matrix m as [n][k], k = 16 ks + 8 h + j (the kernel's k order)."""
-    nt, ks = frag_ntiles(m), s16_ksteps(m)
-    off = s16_offset(m)
-    raw = packed[off: off + nt * ks * 512].view(np.float16).reshape(ks, nt, 2, 2, 32, 8)
-    # [ks][t][part][h][n%32][j] -> [part][t][n%32][ks][h][j]
-    w = raw.transpose(2, 1, 4, 0, 3, 5).reshape(2, nt * 32, ks * 16).astype(np.float64)
+def s16_layer_cols(L):
+    """Natural input column of each k slot (k = 16 ks + 8 h + j) of layer L, or -1."""
+    cols = []
+    for ks in range(s16_layer_ks(L)):
+        m = 8 if L == 8 else (9 if L == 4 and ks >= 16 else L)
+        ksm = ks - 16 if m == 9 else ks
+        cols += [s16_source_col(m, ksm, h, j) for h in range(2) for j in range(8)]
+    return cols
+
+
+def s16_layer(packed, L):
+    """(hi, lo) of layer L as [n][k] in the kernel's k order, decoded from the chunk stream."""
+    G, KS = s16_layer_groups(L), s16_layer_ks(L)
+    off = s16_base() + s16_chunk0(L) * 4096
+    raw = packed[off: off + G * KS // 2 * 4096].view(np.float16)
+    raw = raw.reshape(G, KS // 2, 2, 4, 2, 2, 32, 8)          # g, i, kk, ti, part, h, n, j
+    w = raw.transpose(4, 0, 3, 6, 1, 2, 5, 7).reshape(2, G * 128, KS * 16).astype(np.float64)
     return w[0], w[1]
 
 
-def s16_scales(packed):
-    base = s16_offset(0) + frag_offset(10)
-    return packed[base: base + 10].astype(np.float64), packed[base + 10: base + 20].astype(np.float64)
+def layer_weight(state, L):
+    return (state["dir_linear.weight"] if L == 8 else state[f"pts_linears.{L}.weight"]).numpy().astype(np.float64)
 
 
-def s16_cols(m):
-    return [s16_source_col(m, ks, h, j) for ks in range(s16_ksteps(m)) for h in range(2) for j in range(8)]
-
-
-def test_split_f16_fragments_reconstruct_the_weights(ref_state):
+def test_split_f16_stream_reconstructs_the_weights(ref_state):
     packed = host_pack(ref_state)
-    s_w, inv_w = s16_scales(packed)
-    assert np.all(s_w * inv_w == 1.0)
-    W = {m: ref_state[f"pts_linears.{m}.weight"].numpy().astype(np.float64) for m in range(8)}
-    W[8] = ref_state["dir_linear.weight"].numpy().astype(np.float64)
-    W[9] = W[4]
-    for m in range(10):
-        hi, lo = s16_matrix(packed, m)
-        src = W[m] if m != 9 else W[4]
-        cols = s16_cols(m)
-        ref = np.stack([src[:, c] if c >= 0 else np.zeros(src.shape[0]) for c in cols], 1)
+    c = s16_consts(packed)
+    assert s16_chunk0(9) == 128
+    assert np.all(c["s_w"] * c["inv_w"] == 1.0)
+    for L in range(9):
+        hi, lo = s16_layer(packed, L)
+        W = layer_weight(ref_state, L)
+        cols = s16_layer_cols(L)
+        ref = np.stack([W[:, k] if k >= 0 else np.zeros(W.shape[0]) for k in cols], 1)
         mx = np.abs(ref).max()
-        assert mx * s_w[m] < 2.0 ** 14 and mx * s_w[m] >= 2.0 ** 13, m      # scale puts the max just under 2^14
-        assert np.array_equal(hi, (ref * s_w[m]).astype(np.float32).astype(np.float16).astype(np.float64)), m
-        err = np.abs((hi + lo) * inv_w[m] - ref).max()
-        assert err <= mx * 2.0 ** -23, (m, err)
+        assert 2.0 ** 13 <= mx * c["s_w"][L] < 2.0 ** 14, L      # the scale puts the max just under 2^14
+        assert np.array_equal(hi, (ref * c["s_w"][L]).astype(np.float32).astype(np.float16).astype(np.float64)), L
+        assert np.abs((hi + lo) * c["inv_w"][L] - ref).max() <= mx * 2.0 ** -23, L
+        if L < 8:
+            Wfull = W if L != 8 else W[:, :256]
+            l1 = np.abs(Wfull).sum(1).max()
+            assert l1 <= c["R"][L] <= l1 * 1.001, L               # rigorous bound constant
+            assert c["B"][L] == np.abs(ref_state[f"pts_linears.{L}.bias"].numpy()).max()
 
 
 def emulate_forward_f16x3(packed, x, d, app):
-    """csrc/mlp16.hip's dataflow on the host-packed buffer: per-sample power-of-two scales, f16
-    hi/lo split in float32, the three products accumulated in float64."""
-    s_w, inv_w = s16_scales(packed)
+    """csrc/mlp16.hip's dataflow on the host-packed buffer: per-sample power-of-two scales from the
+    bound R max|a| + B, f16 hi/lo split in float32, the three products accumulated in float64."""
+    c = s16_consts(packed)
     f32 = np.float32
 
     def split(v):
@@ -246,35 +261,39 @@ def emulate_forward_f16x3(packed, x, d, app):
         lo = (v - hi.astype(f32)).astype(np.float16)
         return hi.astype(np.float64), lo.astype(np.float64)
 
-    def scale_of(mx):
-        e = np.frexp(mx.astype(f32))[1]
+    def scale_of(bound):
+        e = np.frexp(bound.astype(f32))[1]
         return np.ldexp(1.0, 14 - e)
 
-    def dense(m, a_cols, s):
-        hi, lo = s16_matrix(packed, m)
+    def dense(L, a_cols, s):
+        hi, lo = s16_layer(packed, L)
         ah, al = split(a_cols * s[:, None])
-        return ah @ hi.T + al @ hi.T + ah @ lo.T
+        assert np.abs(ah).max() < 2.0 ** 15
+        return (ah @ hi.T + al @ hi.T + ah @ lo.T) / (c["s_w"][L] * s)[:, None]
 
     enc = O.positional_encoding(torch.from_numpy(x), 10).numpy().astype(np.float64)
-    pe_cols = np.stack([enc[:, c] if c >= 0 else np.zeros(len(x)) for c in s16_cols(0)], 1)
     m_pe = np.maximum(1.0, np.abs(x).max(1).astype(np.float64))
-    off_bias = frag_offset(10)
-    bias = packed[off_bias: off_bias + 8 * 256].reshape(8, 256).astype(np.float64)
+    bias = packed[frag_offset(10): frag_offset(10) + 8 * 256].reshape(8, 256).astype(np.float64)
+
+    def inputs(L, h):
+        full = np.concatenate([h, enc], 1) if L == 4 else (enc if L == 0 else h)
+        return np.stack([full[:, k] if k >= 0 else np.zeros(len(x)) for k in s16_layer_cols(L)], 1)
+
     s = scale_of(m_pe)
-    y = dense(0, pe_cols, s) / (s_w[0] * s)[:, None] + bias[0]
-    for m in range(1, 8):
+    m_in = m_pe
+    h = None
+    for L in range(8):
+        y = dense(L, inputs(L, h), s) + bias[L]
+        bound = c["R"][L] * m_in + c["B"][L]
         h = np.maximum(y, 0)
-        mx = h.max(1)
-        if m == 4:
-            mx = np.maximum(mx, m_pe)
-        s = scale_of(mx)
-        acc = dense(m, h[:, s16_cols(m)], s)
-        if m == 4:
-            acc += dense(9, np.stack([enc[:, c - 256] if c >= 0 else np.zeros(len(x)) for c in s16_cols(9)], 1), s)
-        y = acc / (s_w[m] * s)[:, None] + bias[m]
-    h = np.maximum(y, 0)
+        assert np.all(np.abs(y).max(1) <= bound)
+        m_in = h.max(1)
+        if L + 1 == 4:
+            bound = np.maximum(bound, m_pe)
+            m_in = np.maximum(m_in, m_pe)
+        s = scale_of(bound)
     p = packed.astype(np.float64)
-    off_sw = off_bias + 8 * 256
+    off_sw = frag_offset(10) + 8 * 256
     off_sb = off_sw + 256
     off_db = off_sb + 4
     off_dwd = off_db + 128
@@ -283,19 +302,18 @@ def emulate_forward_f16x3(packed, x, d, app):
     off_rw = off_ab + 128
     off_rb = off_rw + 3 * 128
     sigma = np.maximum(h @ p[off_sw: off_sw + 256] + p[off_sb], 0)
-    s = scale_of(h.max(1))
     encd = O.positional_encoding(torch.from_numpy(d), 4).numpy().astype(np.float64)
     dvec = p[off_db: off_db + 128] + encd @ p[off_dwd: off_dwd + 128 * 27].reshape(128, 27).T
     appf = np.zeros(128) if app is None else p[off_ab: off_ab + 128] + app.astype(np.float64) @ \
         p[off_aw: off_aw + 128 * 32].reshape(128, 32).T
-    hd = np.maximum(dense(8, h[:, s16_cols(8)], s) / (s_w[8] * s)[:, None] + dvec, 0) + appf
+    hd = np.maximum(dense(8, inputs(8, h), s) + dvec, 0) + appf
     rgb = 1 / (1 + np.exp(-(hd @ p[off_rw: off_rw + 384].reshape(3, 128).T + p[off_rb: off_rb + 3])))
     return rgb, sigma[:, None]
 
 
 def test_emulated_f16x3_kernel_matches_oracle(ref_state, app_vec):
     """The split arithmetic is fp32-accurate: the emulated f16x3 dataflow sits within the
-    parity tolerance of the oracle (and, per element, as close to a float64 evaluation as fp32)."""
+    parity tolerance of the oracle and, per element, as close to a float64 evaluation as fp32."""
     packed = host_pack(ref_state)
     torch.manual_seed(5)
     x = torch.randn(256, 3) * 2
