@@ -161,20 +161,50 @@ __device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand
   });
 }
 
+// VALU instructions to place in each MFMA gap of half-step HS of a group whose side work is of
+// kind KIND (see the side lambdas below): one quarter-tile conversion is ~40 VALU instructions,
+// spread over the 12 MFMA gaps of the half-step (an MFMA of 32 cycles hides ~5 single-issue VALU
+// instructions; bunched, they serialise behind it).
+enum SideKind { kSideNone, kSidePrev, kSideCur, kSideL0, kSideSkipPrev };
+template <int KIND>
+__device__ __forceinline__ constexpr int side_quarters(int hs) {
+  if constexpr (KIND == kSidePrev) return hs == 0 ? 2 : (hs <= 14 ? 1 : 0);
+  if constexpr (KIND == kSideSkipPrev) return hs == 0 ? 2 : (hs <= 18 ? 1 : 0);   // + PE operands at 15..18
+  if constexpr (KIND == kSideCur) return hs == 15 ? 2 : (hs >= 1 && hs <= 14 ? 1 : 0);
+  if constexpr (KIND == kSideL0) return 4;
+  return 0;
+}
+template <int KIND>
+__device__ __forceinline__ constexpr int side_vpg(int hs) {
+  const int q = side_quarters<KIND>(hs);
+  return q == 0 ? 0 : (q * 40 + 11) / 12;
+}
+
 // Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
-// (into `ar`, from `slot_r`) and the side work (VALU) interleaved: 2 ds_read_b128 between
-// consecutive tiles' 3 MFMAs; the VALU fills the MFMA shadow.
-template <int G, bool FIRST, bool READ, int KK_R, typename Side>
+// (into `ar`, from `slot_r`) and the side work (VALU) interleaved: per MFMA gap one ds_read_b128
+// (8 of the 12 gaps) and VPG VALU instructions.
+template <int G, bool FIRST, bool READ, int KK_R, int VPG, typename Side>
 __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
                                           const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side) {
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
   mfma_kstep<G, FIRST>(am, b, acc);
   side();
+#ifdef NERF16_BUNCHED_SIDE   // the previous schedule: reads paired between tiles, VALU left to the compiler
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if constexpr (READ) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                      // 3 MFMAs
   }
+#else
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // 1 MFMA
+    if constexpr (READ) {
+      if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // 1 DS read
+    }
+    if constexpr (VPG > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VPG VALU
+  }
+#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -184,13 +214,13 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
 //   the slot chunk c-1 used | MFMA k-step 1, reading chunk c+1's k-step-0 A
 // On entry chunk c is published, c+1 and c+2 are in flight and a0 holds k-step 0's fragments.
 // TAIL = chunks left after c, capped at 3: the stream's last steps stop loading and waiting.
-template <int G, int SLOT, bool FIRST, int TAIL, typename Side0, typename Side1>
+template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, typename Side0, typename Side1>
 __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int c, float* lds, uint32_t lds_dma,
                                            uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
                                            const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
                                            Side1&& side1) {
   wait_lgkm0();                                     // a0's reads (interleaved in the last half-step) are in
-  half_step<G, FIRST, true, 1>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0);
+  half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0);
 #ifndef NERF16_T_NOBARRIER
   if constexpr (TAIL >= 1) {
     wait_vmcnt<TAIL >= 2 ? 4 : 0>();
@@ -199,20 +229,21 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
 #endif
   if constexpr (TAIL >= 3) chunk_dma<(SLOT + 3) & 3>(stream, c + 3, lds_dma, voff);
   wait_lgkm0();                                     // a1's reads are in
-  half_step<G, false, (TAIL >= 1), 0>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0, lane, side1);
+  half_step<G, false, (TAIL >= 1), 0, side_vpg<KIND>(HS0 + 1)>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0,
+                                                            lane, side1);
 }
 
 // A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
 // the B operand of k-step 2i+kk; side(i, kk) is the VALU work placed in that half-step.
 // TAIL_END = chunks after this group (capped at 3).
-template <int G, int NSTEP, int SLOT0, int TAIL_END, typename Opnd, typename Side>
+template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, typename Opnd, typename Side>
 __device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
                                           uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], f32x16 (&acc)[8],
                                           int lane, Opnd&& operand, Side&& side) {
   static_for<NSTEP>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     constexpr int left = NSTEP - 1 - i + TAIL_END;
-    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3)>(
+    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i>(
         stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
         operand(ic, std::integral_constant<int, 1>{}), acc, lane,
         [&]() __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}); },
@@ -221,24 +252,22 @@ __device__ __forceinline__ void run_group(const float* __restrict__ stream, int 
 }
 
 // ---- epilogue pieces (the side work) ----------------------------------------------------------
-// Registers 8SH..8SH+7 of output tile T -> the next layer's operand `op`:
+// Quarter QG (0..15) of a 4-tile group = registers 4q..4q+3 (q = QG % 4) of output tile T0 + QG / 4
+// -> elements 4(q & 1) .. +3 of the next layer's operand in[OP0 + QG / 2]:
 //   y = acc*inv + bias, r = ReLU(y), op = split(r*s); m tracks max r; SIGMA adds ws . r to part.
-template <int T, int SH, bool SIGMA>
-__device__ __forceinline__ void convert8(const f32x16 (&acc)[8], float inv, const float* bias, float s, Operand& op,
-                                         float& m, float& part, const float* ws, int h) {
+template <int T0, int OP0, int QG, bool SIGMA>
+__device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const float* bias, float s,
+                                         Operand (&in)[16], float& m, float& part, const float* ws, int h) {
+  constexpr int T = T0 + QG / 4, q = QG % 4;
+  const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
+  f32x4 w;
+  if constexpr (SIGMA) w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
 #pragma unroll
-  for (int qq = 0; qq < 2; ++qq) {
-    const int q = 2 * SH + qq;
-    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
-    f32x4 w;
-    if constexpr (SIGMA) w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float r = fmaxf(fmaf(acc[T][8 * SH + 4 * qq + e], inv, b[e]), 0.0f);
-      m = fmaxf(m, r);
-      if constexpr (SIGMA) part = fmaf(w[e], r, part);
-      split_into(r * s, op, 4 * qq + e);
-    }
+  for (int e = 0; e < 4; ++e) {
+    const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, b[e]), 0.0f);
+    m = fmaxf(m, r);
+    if constexpr (SIGMA) part = fmaf(w[e], r, part);
+    split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
   }
 }
 
@@ -340,26 +369,31 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   // ---- layer 0: PE(63) -> 256, 2 chunk-steps per group ----
   auto pe_operand_of = [&](auto i, auto kk) -> const Operand& { return pe_op[kstep_of(i, kk)]; };
-  run_group<0, 2, 0, 3>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
-  // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE)
-  run_group<1, 2, 2, 3>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
-                        [&](auto i, auto kk) __attribute__((always_inline)) {
-                          constexpr int t = kstep_of(i, kk);   // tiles 0..3
-                          convert8<t, 0, false>(acc, inv_cur, bias, s_nxt, in[2 * t], m, part, ws, h);
-                          convert8<t, 1, false>(acc, inv_cur, bias, s_nxt, in[2 * t + 1], m, part, ws, h);
-                        });
+  run_group<0, 2, 0, 3, kSideNone>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
+  // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE),
+  // 4 quarters per half-step
+  run_group<1, 2, 2, 3, kSideL0>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
+                                 [&](auto i, auto kk) __attribute__((always_inline)) {
+                                   constexpr int hs = kstep_of(i, kk);
+                                   static_for<4>([&](auto qc) __attribute__((always_inline)) {
+                                     convert4<0, 0, 4 * hs + decltype(qc)::value, false>(acc, inv_cur, bias, s_nxt, in,
+                                                                                      m, part, ws, h);
+                                   });
+                                 });
   STAMP16(2);
 
   // ---- layers 1..7 ----
   // On entry to layer L: operands 0..7 hold y_{L-1} tiles 0-3 split at s_cur, y_{L-1} tiles 4-7
   // wait in acc[4..7], m holds the max of ReLU(y_{L-1}) tiles 0-3.
   //
-  // Side-work schedule, by half-step hs = 2*(chunk-step) + k-step-in-chunk (one half-tile
-  // conversion every other half-step, so the VALU stays inside the MFMA shadow):
-  //  * group A converts y_{L-1} tile 4+i half sh into operand 8+2i+sh at hs = 4i + 2sh; that
-  //    operand is first read at hs = 8+2i+sh, and acc[4..7] is free again before group B;
-  //  * group B converts y_L tile t half sh into operand 2t+sh at hs = 4t + 2sh + 1; that operand
-  //    was last read at hs = 2t+sh, and is next read at the next layer's hs = 2t+sh.
+  // Side-work schedule, by half-step hs of a group (one k-step), in quarter tiles (4 registers of a
+  // tile, ~40 VALU instructions, spread over the half-step's 12 MFMA gaps):
+  //  * group A converts y_{L-1} tiles 4-7 into operands 8..15: quarters 0, 1 at hs 0, quarter
+  //    hs + 1 at hs 1..14.  Operand 8+j (quarters 2j, 2j+1) is complete at hs 2j and first read at
+  //    hs 8+j; acc[4..7] is free again before group B;
+  //  * group B converts this layer's y_L tiles 0-3 into operands 0..7: quarter hs - 1 at hs 1..14,
+  //    quarters 14, 15 at hs 15.  Operand j was last read at hs j, and is next read at the next
+  //    layer's hs j.
   float inv_prev = inv_cur;
   const float* bias_prev = bias;
   s_cur = s_nxt;
@@ -372,17 +406,23 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // group A's side: y_{L-1} tiles 4-7 (SIGMA: also the density head's dot product)
   auto side_prev = [&](auto i, auto kk, auto sigma_tag) __attribute__((always_inline)) {
     constexpr int hs = kstep_of(i, kk);
-    if constexpr (hs % 2 == 0 && hs < 16) {
-      constexpr int t = 4 + hs / 4, sh = (hs / 2) % 2;
-      convert8<t, sh, decltype(sigma_tag)::value>(acc, inv_prev, bias_prev, s_cur, in[2 * t + sh], m, part, ws, h);
+    constexpr bool sg = decltype(sigma_tag)::value;
+    if constexpr (hs == 0) {
+      convert4<4, 8, 0, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
+      convert4<4, 8, 1, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
+    } else if constexpr (hs <= 14) {
+      convert4<4, 8, hs + 1, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
     }
   };
   // group B's side: this layer's y_L tiles 0-3
   auto side_cur = [&](auto i, auto kk, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
     constexpr int hs = kstep_of(i, kk);
-    if constexpr (hs % 2 == 1 && hs < 16) {
-      constexpr int t = hs / 4, sh = (hs / 2) % 2;
-      convert8<t, sh, decltype(sigma_tag)::value>(acc, inv_cur, bias_l, s_nxt, in[2 * t + sh], m, part, ws, h);
+    constexpr bool sg = decltype(sigma_tag)::value;
+    if constexpr (hs >= 1 && hs <= 14) {
+      convert4<0, 0, hs - 1, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
+    } else if constexpr (hs == 15) {
+      convert4<0, 0, 14, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
+      convert4<0, 0, 15, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
     }
   };
   using NoSigma = std::false_type;
@@ -394,16 +434,17 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
     // group A (k-steps 0..15, + PE 16..19 at layer 4)
     if (L == kSkipLayer) {
-      // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur in the free odd half-steps
-      // 1, 3, 5, 7 (read from hs 16)
-      run_group<0, 10, 0, 3>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
-                             [&](auto i, auto kk) __attribute__((always_inline)) {
-                               constexpr int hs = kstep_of(i, kk);
-                               side_prev(i, kk, NoSigma{});
-                               if constexpr (hs % 2 == 1 && hs < 8) pe_operand<hs / 2>(pe_mine, s_cur, pe_op[hs / 2], lane);
-                             });
+      // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
+      // read at hs 16 + q)
+      run_group<0, 10, 0, 3, kSideSkipPrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+                                            [&](auto i, auto kk) __attribute__((always_inline)) {
+                                              constexpr int hs = kstep_of(i, kk);
+                                              side_prev(i, kk, NoSigma{});
+                                              if constexpr (hs >= 15 && hs < 19)
+                                                pe_operand<hs - 15>(pe_mine, s_cur, pe_op[hs - 15], lane);
+                                            });
     } else {
-      run_group<0, 8, 0, 3>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<0, 8, 0, 3, kSidePrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, NoSigma{}); });
     }
     // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
@@ -414,13 +455,13 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     m = 0.0f;
     // group B (layer 7 also starts the density head)
     if (L == kSkipLayer) {
-      run_group<1, 10, 2, 3>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+      run_group<1, 10, 2, 3, kSideCur>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
                              [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
     } else if (L == 7) {
-      run_group<1, 8, 0, 3>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, Sigma{}); });
     } else {
-      run_group<1, 8, 0, 3>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
     }
     inv_prev = inv_cur;
@@ -432,7 +473,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
   // operands 8..15 and finishes the density head ----
   inv_cur = cst[kS16InvW + 8] / s_cur;
-  run_group<0, 8, 0, 0>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+  run_group<0, 8, 0, 0, kSidePrev>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, Sigma{}); });
   STAMP16(10);
 

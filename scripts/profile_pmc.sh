@@ -1,16 +1,17 @@
 #!/bin/bash
 # PMC passes for the bench workload (one counter group per rocprofv3 run, as MI355X_MICROARCH.md
 # prescribes: FETCH_SIZE and WRITE_SIZE do not fit one pass).  Usage (on the GPU box, repo root):
-#   bash scripts/profile_pmc.sh gpurun_out/pmc
+#   bash scripts/profile_pmc.sh gpurun_out/pmc [f16x3|f32]
 set -e
 OUT=${1:-gpurun_out/pmc}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-CMD="python3 $ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+ARITH=${2:-f16x3}
+CMD="python3 $ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --arith $ARITH"
 i=0
-for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "TCC_HIT_sum TCC_MISS_sum"; do
+for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $group --kernel-trace -d "$ROOT/$OUT/p$i" -o run --output-format csv -- $CMD > "$ROOT/$OUT/p$i.log" 2>&1
 done

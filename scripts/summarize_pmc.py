@@ -3,7 +3,7 @@
 Per kernel: average per dispatch of every counter, and for the MLP kernel the HBM-side traffic
 per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; gfx950's FETCH_SIZE reads half the
 bytes of a wide coalesced stream, MI355X_MICROARCH.md §HBM), the clock (GRBM_GUI_ACTIVE / 8 /
-duration) and the MFMA busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles))."""
+duration) and the MFMA busy fraction; the MLP kernel is mlp16_kernel (f16x3) when present, else mlp_kernel (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles))."""
 import collections, csv, glob, json, os, sys
 
 src, out = sys.argv[1], sys.argv[2]
@@ -19,11 +19,13 @@ for k, cs in per.items():
     if not k.startswith("nerf::"):
         continue
     res["kernels"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
-m = res["kernels"].get("nerf::mlp_kernel", {})
+mlp = "nerf::mlp16_kernel" if "nerf::mlp16_kernel" in res["kernels"] else "nerf::mlp_kernel"
+res["mlp_kernel"] = mlp
+m = res["kernels"].get(mlp, {})
 if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
     res["mlp_hbm_bytes_per_launch"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
 if "GRBM_GUI_ACTIVE" in m:
-    ts = [t for (f, _), t in dur["nerf::mlp_kernel"].items() if "/p3/" in f]
+    ts = [t for (f, _), t in dur[mlp].items() if "/p3/" in f]
     avg_t = sum(ts) / len(ts)
     res["mlp_clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8 / avg_t / 1e9
     res["mlp_mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
