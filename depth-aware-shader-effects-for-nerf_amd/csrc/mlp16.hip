@@ -177,7 +177,7 @@ __device__ __forceinline__ constexpr int side_quarters(int hs) {
 template <int KIND>
 __device__ __forceinline__ constexpr int side_vpg(int hs) {
   const int q = side_quarters<KIND>(hs);
-  return q == 0 ? 0 : (q * 40 + 11) / 12;
+  return q == 0 ? 0 : (q * 40 + 10) / 11;
 }
 
 // Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
@@ -186,9 +186,13 @@ __device__ __forceinline__ constexpr int side_vpg(int hs) {
 template <int G, bool FIRST, bool READ, int KK_R, int VPG, typename Side>
 __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
                                           const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side) {
+  // the side work's small LDS reads (bias, density weights) go first: LDS returns in order, so its
+  // VALU then waits for them alone, not for the fragment reads issued after them
+  side(std::integral_constant<int, 0>{});
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
   mfma_kstep<G, FIRST>(am, b, acc);
-  side();
+  side(std::integral_constant<int, 1>{});
 #ifdef NERF16_BUNCHED_SIDE   // the previous schedule: reads paired between tiles, VALU left to the compiler
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -202,7 +206,9 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
     if constexpr (READ) {
       if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // 1 DS read
     }
-    if constexpr (VPG > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VPG VALU
+    if constexpr (VPG > 0) {
+      if (i > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);         // VPG VALU (none in gap 0:
+    }                                                                         // the bias reads land)
   }
 #endif
   __builtin_amdgcn_sched_barrier(0);
@@ -234,7 +240,8 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
 }
 
 // A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
-// the B operand of k-step 2i+kk; side(i, kk) is the VALU work placed in that half-step.
+// the B operand of k-step 2i+kk; side(i, kk, phase) is the VALU work placed in that half-step:
+// phase 0 issues its LDS reads, phase 1 computes.
 // TAIL_END = chunks after this group (capped at 3).
 template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, typename Opnd, typename Side>
 __device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
@@ -246,8 +253,8 @@ __device__ __forceinline__ void run_group(const float* __restrict__ stream, int 
     chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i>(
         stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
         operand(ic, std::integral_constant<int, 1>{}), acc, lane,
-        [&]() __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}); },
-        [&]() __attribute__((always_inline)) { side(ic, std::integral_constant<int, 1>{}); });
+        [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}, ph); },
+        [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 1>{}, ph); });
   });
 }
 
@@ -255,35 +262,56 @@ __device__ __forceinline__ void run_group(const float* __restrict__ stream, int 
 // Quarter QG (0..15) of a 4-tile group = registers 4q..4q+3 (q = QG % 4) of output tile T0 + QG / 4
 // -> elements 4(q & 1) .. +3 of the next layer's operand in[OP0 + QG / 2]:
 //   y = acc*inv + bias, r = ReLU(y), op = split(r*s); m tracks max r; SIGMA adds ws . r to part.
-template <int T0, int OP0, int QG, bool SIGMA>
-__device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const float* bias, float s,
-                                         Operand (&in)[16], float& m, float& part, const float* ws, int h) {
+// Phase 0 (load4) reads the quarter's bias (and density weights) from LDS into `qv`; phase 1
+// (convert4) computes.
+struct QuarterVec {
+  f32x4 b, w;
+};
+template <int T0, int QG, bool SIGMA>
+__device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
-  const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
-  f32x4 w;
-  if constexpr (SIGMA) w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
+  qv.b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
+  if constexpr (SIGMA) qv.w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
+}
+template <int T0, int OP0, int QG, bool SIGMA>
+__device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const QuarterVec& qv, float s,
+                                         Operand (&in)[16], float& m, float& part) {
+  constexpr int T = T0 + QG / 4, q = QG % 4;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, b[e]), 0.0f);
+    const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, qv.b[e]), 0.0f);
     m = fmaxf(m, r);
-    if constexpr (SIGMA) part = fmaf(w[e], r, part);
+    if constexpr (SIGMA) part = fmaf(qv.w[e], r, part);
     split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
   }
 }
+// Phase PH of quarter QG (slot J of this half-step's quarter vectors).
+template <int PH, int T0, int OP0, int QG, bool SIGMA>
+__device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const float* bias, const float* ws, int h,
+                                        float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv) {
+  if constexpr (PH == 0) load4<T0, QG, SIGMA>(bias, ws, h, qv);
+  else convert4<T0, OP0, QG, SIGMA>(acc, inv, qv, s, in, m, part);
+}
 
-// PE operand Q split at scale s from this wave's LDS copy (layer 4 reads [h3, enc_x]).
-template <int Q>
-__device__ __forceinline__ void pe_operand(const float* pe_mine, float s, Operand& op, int lane) {
+// PE operand Q split at scale s from this wave's LDS copy (layer 4 reads [h3, enc_x]): phase 0
+// reads the 8 values into `v`, phase 1 splits them.
+template <int PH, int Q>
+__device__ __forceinline__ void pe_operand(const float* pe_mine, float s, Operand& op, float (&v)[8], int lane) {
+  if constexpr (PH == 0) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) split_into(pe_mine[(8 * Q + j) * 64 + lane] * s, op, j);
+    for (int j = 0; j < 8; ++j) v[j] = pe_mine[(8 * Q + j) * 64 + lane];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split_into(v[j] * s, op, j);
+  }
 }
 
 // The sample's max over both lane halves.
 __device__ __forceinline__ float sample_max(float m) { return fmaxf(m, __shfl_xor(m, 32)); }
 
 struct NoSide {
-  template <typename A, typename B>
-  __device__ __forceinline__ void operator()(A, B) const {}
+  template <typename A, typename B, typename C>
+  __device__ __forceinline__ void operator()(A, B, C) const {}
 };
 
 template <typename I, typename K>
@@ -372,12 +400,15 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   run_group<0, 2, 0, 3, kSideNone>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
   // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE),
   // 4 quarters per half-step
+  QuarterVec qv[4];
+  float pe_v[8];
   run_group<1, 2, 2, 3, kSideL0>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
-                                 [&](auto i, auto kk) __attribute__((always_inline)) {
+                                 [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
                                    constexpr int hs = kstep_of(i, kk);
                                    static_for<4>([&](auto qc) __attribute__((always_inline)) {
-                                     convert4<0, 0, 4 * hs + decltype(qc)::value, false>(acc, inv_cur, bias, s_nxt, in,
-                                                                                      m, part, ws, h);
+                                     constexpr int j = decltype(qc)::value;
+                                     quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false>(
+                                         acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j]);
                                    });
                                  });
   STAMP16(2);
@@ -404,25 +435,25 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     else return pe_op[ks - 16];
   };
   // group A's side: y_{L-1} tiles 4-7 (SIGMA: also the density head's dot product)
-  auto side_prev = [&](auto i, auto kk, auto sigma_tag) __attribute__((always_inline)) {
-    constexpr int hs = kstep_of(i, kk);
+  auto side_prev = [&](auto i, auto kk, auto ph, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs == 0) {
-      convert4<4, 8, 0, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
-      convert4<4, 8, 1, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
+      quarter<P, 4, 8, 0, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0]);
+      quarter<P, 4, 8, 1, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1]);
     } else if constexpr (hs <= 14) {
-      convert4<4, 8, hs + 1, sg>(acc, inv_prev, bias_prev, s_cur, in, m, part, ws, h);
+      quarter<P, 4, 8, hs + 1, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0]);
     }
   };
   // group B's side: this layer's y_L tiles 0-3
-  auto side_cur = [&](auto i, auto kk, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
-    constexpr int hs = kstep_of(i, kk);
+  auto side_cur = [&](auto i, auto kk, auto ph, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs >= 1 && hs <= 14) {
-      convert4<0, 0, hs - 1, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
+      quarter<P, 0, 0, hs - 1, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0]);
     } else if constexpr (hs == 15) {
-      convert4<0, 0, 14, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
-      convert4<0, 0, 15, sg>(acc, inv_cur, bias_l, s_nxt, in, m, part, ws, h);
+      quarter<P, 0, 0, 14, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0]);
+      quarter<P, 0, 0, 15, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1]);
     }
   };
   using NoSigma = std::false_type;
@@ -437,15 +468,16 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
       // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
       // read at hs 16 + q)
       run_group<0, 10, 0, 3, kSideSkipPrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
-                                            [&](auto i, auto kk) __attribute__((always_inline)) {
+                                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
                                               constexpr int hs = kstep_of(i, kk);
-                                              side_prev(i, kk, NoSigma{});
+                                              side_prev(i, kk, ph, NoSigma{});
                                               if constexpr (hs >= 15 && hs < 19)
-                                                pe_operand<hs - 15>(pe_mine, s_cur, pe_op[hs - 15], lane);
+                                                pe_operand<decltype(ph)::value, hs - 15>(pe_mine, s_cur, pe_op[hs - 15],
+                                                                                         pe_v, lane);
                                             });
     } else {
       run_group<0, 8, 0, 3, kSidePrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                            [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, NoSigma{}); });
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, NoSigma{}); });
     }
     // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
     m = sample_max(m);
@@ -456,13 +488,13 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     // group B (layer 7 also starts the density head)
     if (L == kSkipLayer) {
       run_group<1, 10, 2, 3, kSideCur>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
-                             [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
+                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
     } else if (L == 7) {
       run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                            [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, Sigma{}); });
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, Sigma{}); });
     } else {
       run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                            [&](auto i, auto kk) __attribute__((always_inline)) { side_cur(i, kk, bias_l, NoSigma{}); });
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
     }
     inv_prev = inv_cur;
     bias_prev = bias_l;
@@ -474,7 +506,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // operands 8..15 and finishes the density head ----
   inv_cur = cst[kS16InvW + 8] / s_cur;
   run_group<0, 8, 0, 0, kSidePrev>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                        [&](auto i, auto kk) __attribute__((always_inline)) { side_prev(i, kk, Sigma{}); });
+                        [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
   STAMP16(10);
 
   // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.

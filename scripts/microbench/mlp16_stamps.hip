@@ -15,7 +15,7 @@ int main() {
   const int64_t R = 640000, N = 64, M = R * N;
   std::vector<float> h(nerf::kPackedFloats);
   srand(1);
-  for (auto& v : h) v = ((float)rand() / RAND_MAX - 0.5f) * 0.1f;
+  for (auto& v : h) v = ((float)rand() / (float)RAND_MAX - 0.5f) * 0.1f;
   for (int L = 0; L < nerf::kS16Layers; ++L) {
     h[nerf::kOffScale16 + nerf::kS16Sw + L] = 65536.f;
     h[nerf::kOffScale16 + nerf::kS16InvW + L] = 1.f / 65536.f;
