@@ -121,6 +121,26 @@ __device__ __forceinline__ void chunk_dma(const float* __restrict__ stream, int 
   }
 }
 
+// Piece i (0..3) of this wave's share of chunk c into LDS slot SLOT.
+template <int SLOT, int I>
+__device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
+                                                uint32_t voff) {
+#ifdef NERF16_T_NODMA
+  return;
+#endif
+  const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(src + I * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + I * (kW16Waves * 1024))
+      : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -144,8 +164,8 @@ __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], 
 }
 
 // One k-step of group G (tiles 4G .. 4G+3).
-template <int G, bool FIRST>
-__device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8]) {
+template <int G, bool FIRST, typename Hook>
+__device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8], Hook&& hook) {
 #ifdef NERF16_T_NOMFMA   // timing-only builds (scripts/microbench/mlp16_stamps.hip); wrong results
 #pragma unroll
   for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[4 * G + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
@@ -158,6 +178,7 @@ __device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand
     else c = mfma16(a[i][1], b.hi, acc[4 * G + i]);
     c = mfma16(a[i][0], b.lo, c);
     acc[4 * G + i] = mfma16(a[i][0], b.hi, c);
+    hook(ic);
   });
 }
 
@@ -183,15 +204,16 @@ __device__ __forceinline__ constexpr int side_vpg(int hs) {
 // Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
 // (into `ar`, from `slot_r`) and the side work (VALU) interleaved: per MFMA gap one ds_read_b128
 // (8 of the 12 gaps) and VPG VALU instructions.
-template <int G, bool FIRST, bool READ, int KK_R, int VPG, typename Side>
+template <int G, bool FIRST, bool READ, int KK_R, int VPG, typename Side, typename Hook>
 __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
-                                          const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side) {
+                                          const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side,
+                                          Hook&& hook) {
   // the side work's small LDS reads (bias, density weights) go first: LDS returns in order, so its
   // VALU then waits for them alone, not for the fragment reads issued after them
   side(std::integral_constant<int, 0>{});
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
-  mfma_kstep<G, FIRST>(am, b, acc);
+  mfma_kstep<G, FIRST>(am, b, acc, hook);
   side(std::integral_constant<int, 1>{});
 #ifdef NERF16_BUNCHED_SIDE   // the previous schedule: reads paired between tiles, VALU left to the compiler
 #pragma unroll
@@ -226,17 +248,25 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
                                            const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
                                            Side1&& side1) {
   wait_lgkm0();                                     // a0's reads (interleaved in the last half-step) are in
-  half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0);
+  half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
+                                                    [](auto) {});
 #ifndef NERF16_T_NOBARRIER
   if constexpr (TAIL >= 1) {
     wait_vmcnt<TAIL >= 2 ? 4 : 0>();
     __builtin_amdgcn_s_barrier();
   }
 #endif
-  if constexpr (TAIL >= 3) chunk_dma<(SLOT + 3) & 3>(stream, c + 3, lds_dma, voff);
   wait_lgkm0();                                     // a1's reads are in
+  // DMA of chunk c+3 into the slot chunk c-1 used: one piece after each tile's MFMAs
+  auto dma = [&](auto ti) __attribute__((always_inline)) {
+#ifdef NERF16_DMA_BUNCHED
+    if constexpr (TAIL >= 3 && decltype(ti)::value == 0) chunk_dma<(SLOT + 3) & 3>(stream, c + 3, lds_dma, voff);
+#else
+    if constexpr (TAIL >= 3) chunk_dma_piece<(SLOT + 3) & 3, decltype(ti)::value>(stream, c + 3, lds_dma, voff);
+#endif
+  };
   half_step<G, false, (TAIL >= 1), 0, side_vpg<KIND>(HS0 + 1)>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0,
-                                                            lane, side1);
+                                                            lane, side1, dma);
 }
 
 // A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
