@@ -33,6 +33,7 @@
 // ring three chunks ahead, published by a counted vmcnt wait + barrier, and read back by all
 // four waves with ds_read_b128 interleaved between the MFMAs.
 #include "common.h"
+#include "pe_sin.h"
 
 namespace nerf {
 
@@ -247,7 +248,9 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
                                            uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
                                            const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
                                            Side1&& side1) {
+#ifdef NERF16_EXPLICIT_LGKM
   wait_lgkm0();                                     // a0's reads (interleaved in the last half-step) are in
+#endif
   half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
                                                     [](auto) {});
 #ifndef NERF16_T_NOBARRIER
@@ -256,7 +259,9 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
     __builtin_amdgcn_s_barrier();
   }
 #endif
+#ifdef NERF16_EXPLICIT_LGKM
   wait_lgkm0();                                     // a1's reads are in
+#endif
   // DMA of chunk c+3 into the slot chunk c-1 used: one piece after each tile's MFMAs
   auto dma = [&](auto ti) __attribute__((always_inline)) {
 #ifdef NERF16_DMA_BUNCHED
@@ -319,6 +324,13 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
 template <int PH, int T0, int OP0, int QG, bool SIGMA>
 __device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const float* bias, const float* ws, int h,
                                         float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv) {
+#ifdef NERF16_T_NOSIDE   // timing-only builds: no epilogue conversions (one register kept live); wrong results
+  if constexpr (PH == 1) {
+    constexpr int T = T0 + QG / 4, q = QG % 4;
+    asm volatile("" : "+v"(in[OP0 + QG / 2].hi) : "v"(acc[T][4 * q]));
+  }
+  return;
+#endif
   if constexpr (PH == 0) load4<T0, QG, SIGMA>(bias, ws, h, qv);
   else convert4<T0, OP0, QG, SIGMA>(acc, inv, qv, s, in, m, part);
 }
@@ -385,15 +397,25 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   chunk_dma<2>(stream, 2, lds_dma, voff);
 
   // PE in layout.h::pe_feature order (models.py:36-44): sin on lane half 0, cos on half 1.
+  // pe_sin.h: one reduction + both polynomials per value; a wave with a coordinate beyond its
+  // range (|x| 2^9 > kPeSinMax) takes the library sincosf.
   float pe[kPeSteps];
+  const float ax = fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2])));
+  if (__any(ax * (float)(1 << (kPosLevels - 1)) > kPeSinMax)) {
 #pragma unroll
-  for (int i = 0; i < kPosLevels; ++i)
+    for (int i = 0; i < kPosLevels; ++i)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      float sn, cs;
-      sincosf(x[c] * (float)(1 << i), &sn, &cs);
-      pe[3 * i + c] = h ? cs : sn;
-    }
+      for (int c = 0; c < 3; ++c) {
+        float sn, cs;
+        sincosf(x[c] * (float)(1 << i), &sn, &cs);
+        pe[3 * i + c] = h ? cs : sn;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kPosLevels; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pe[3 * i + c] = pe_sin_reduced(x[c] * (float)(1 << i), h);
+  }
   pe[30] = h ? x[1] : x[0];
   pe[31] = h ? 0.0f : x[2];
   float* pe_mine = lds + kLdsPe + wave * kPeSteps * 64;
