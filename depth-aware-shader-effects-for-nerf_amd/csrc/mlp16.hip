@@ -87,7 +87,11 @@ constexpr int kLdsBias = kLdsPe + kW16Waves * kPeSteps * 64;
 constexpr int kLdsSigmaW = kLdsBias + 8 * kHidden;
 constexpr int kLdsVecFloats = 8 * kHidden + kHidden + 4;    // kOffBias .. kOffSigmaB + 4, contiguous in `packed`
 constexpr int kLdsConsts = kLdsBias + kLdsVecFloats;
-constexpr int kLdsFloats = kLdsConsts + kS16Consts;          // 105 KiB
+constexpr int kLdsRgb = kLdsConsts + kS16Consts;             // rgb_linear weight (3 x 128) + bias (4)
+constexpr int kLdsRgbFloats = 3 * kDirHidden + 4;
+constexpr int kLdsFeat = kLdsRgb + kLdsRgbFloats;             // per wave: its ray's features (256)
+constexpr int kLdsFloats = kLdsFeat + kW16Waves * kRayFeat;   // 111 KiB
+static_assert(kOffRgbB == kOffRgbW + 3 * kDirHidden && kLdsRgb % 4 == 0 && kLdsFeat % 4 == 0, "LDS vector layout");
 static_assert(kOffSigmaW == kOffBias + 8 * kHidden && kOffSigmaB == kOffSigmaW + kHidden, "packed vector order");
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -387,6 +391,9 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   for (int i = threadIdx.x; i < kLdsVecFloats / 4; i += 64 * kW16Waves)
     reinterpret_cast<f32x4*>(lds + kLdsBias)[i] = reinterpret_cast<const f32x4*>(packed + kOffBias)[i];
   if (threadIdx.x < kS16Consts) lds[kLdsConsts + threadIdx.x] = packed[kOffScale16 + threadIdx.x];
+  if (threadIdx.x < kLdsRgbFloats / 4)
+    reinterpret_cast<f32x4*>(lds + kLdsRgb)[threadIdx.x] = reinterpret_cast<const f32x4*>(packed + kOffRgbW)[threadIdx.x];
+  const int slot = out_slot && valid ? out_slot[s] : 0;
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_sched_barrier(0);
   const float* stream = packed + kOff16;
@@ -556,6 +563,25 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
   // operands 8..15 and finishes the density head ----
+  // When N is a multiple of 32 the wave's 32 samples lie on one ray: its 1 KiB of ray features
+  // (b_dir + W_dd PE(d) | appearance) is DMA'd into this wave's LDS area while the colour layer
+  // runs (the stream's last vmcnt(0) covers it), so the heads read LDS, not HBM.
+  const bool one_ray = (N & 31) == 0;
+  float* feat_mine = lds + kLdsFeat + wave * kRayFeat;
+  if (one_ray) {
+    const char* src = reinterpret_cast<const char*>(feat + (imin64(s0, M - 1) / N) * kRayFeat);   // tail waves: last ray
+    const uint32_t dst = (uint32_t)(uintptr_t)(lptr_t)feat_mine;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(16u * lane), "s"(src), "s"(dst)
+        : "memory");
+  }
   inv_cur = cst[kS16InvW + 8] / s_cur;
   run_group<0, 8, 0, 0, kSidePrev>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
@@ -565,33 +591,40 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
   // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
   // (models.py:141-156); the bracket and the appearance part come per ray in `feat`.
-  const float* fr = feat + r * kRayFeat;
-  const float* wr = packed + kOffRgbW;
+  const float* wr = lds + kLdsRgb;
   float pr[3] = {0.0f, 0.0f, 0.0f};
+  auto colour_head = [&](const float* fr) __attribute__((always_inline)) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 fd = *reinterpret_cast<const f32x4*>(fr + t * 32 + 8 * q + 4 * h);
-      const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
-      float hd[4];
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 fd = *reinterpret_cast<const f32x4*>(fr + t * 32 + 8 * q + 4 * h);
+        const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
+        float hd[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f) + ap[e];
+        for (int e = 0; e < 4; ++e) hd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f) + ap[e];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
+        for (int c = 0; c < 3; ++c) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], hd[e], pr[c]);
+          for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], hd[e], pr[c]);
+        }
       }
-    }
+  };
+  if (one_ray) {
+    wait_vmcnt<0>();
+    colour_head(feat_mine);
+  } else {
+    colour_head(feat + r * kRayFeat);
+  }
   float out[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float v = pr[c] + __shfl_xor(pr[c], 32) + packed[kOffRgbB + c];
+    const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
     out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
   }
   if (h == 0 && valid) {
-    const int64_t o_s = out_slot ? r * out_T + out_slot[s] : s;
+    const int64_t o_s = out_slot ? r * out_T + slot : s;
     sigma[o_s] = sig;
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
