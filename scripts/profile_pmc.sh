@@ -9,9 +9,10 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 ARITH=${2:-f16x3}
-CMD="python3 $ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --arith $ARITH"
+CMD="python3 $ROOT/bench.py --steps ${STEPS:-1} --warmup ${WARMUP:-0} --no-cpu-baseline --arith $ARITH"
 i=0
 for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))
+  case " ${PASSES:-1 2 3 4 5 6} " in *" $i "*) ;; *) continue ;; esac
   timeout -k 10 300 rocprofv3 --pmc $group --kernel-trace -d "$ROOT/$OUT/p$i" -o run --output-format csv -- $CMD > "$ROOT/$OUT/p$i.log" 2>&1
 done
