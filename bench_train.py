@@ -15,7 +15,9 @@ Rank 0 prints one JSON line; value = rays trained per second over all ranks (wea
 
 roofline: per-sample algorithmic FLOP of the three MFMA kernels (forward 1,048,832; data
 gradients 983,040; weight gradients 1,066,752 including bias columns — DESIGN.md §Training)
-over their event-timed durations; peak = fp32 MFMA dense 157.3 TFLOP/s.
+over their event-timed durations.  The forward runs on the MLP arithmetic selected by --arith
+(f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
+157.3); the data- and weight-gradient kernels run on fp32 MFMA (peak 157.3 TFLOP/s).
 cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on a 1024-ray
 batch on this host's cores.
 """
@@ -46,6 +48,7 @@ def parse():
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="forward MLP MFMA arithmetic")
     return p.parse_args()
 
 
@@ -88,6 +91,7 @@ def main():
     from nerfmi import _lib
     from nerfmi.dataset import SyntheticNeRFDataset
     from nerfmi.train import Trainer
+    nerfmi.set_mlp_arith(args.arith)
     cfg = nerfmi.Config()
     np.random.seed(100 + rank)                    # each rank draws its own images / pixels
     ds = SyntheticNeRFDataset(cfg, n_images=100)
@@ -147,6 +151,8 @@ def main():
         rays = args.batch * args.steps * world
         kern = {"mlp_forward_train": (FLOP_FWD, kt["mlp_forward_ms"]), "mlp_backward": (FLOP_DGRAD, kt["mlp_backward_ms"]),
                 "wgrad": (FLOP_WGRAD, kt["param_grads_ms"])}
+        peaks = {"mlp_forward_train": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
+                 "mlp_backward": MFMA_F32_PEAK_TFLOPS, "wgrad": MFMA_F32_PEAK_TFLOPS}
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]
         ach = M * flop / (ms * 1e-3) / 1e12
@@ -158,10 +164,12 @@ def main():
                        "pre-generated in HBM; student = torch.manual_seed(0); NeRF(Config())",
                "config": {"workload": "chair-style training loop, one image per batch", "rays_per_gpu_per_step":
                           args.batch, "n_samples": cfg.num_samples, "parallelism": f"dp{world} (RCCL all-reduce)"},
-               "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": MFMA_F32_PEAK_TFLOPS,
-                            "unit": "TFLOP/s", "frac": ach / MFMA_F32_PEAK_TFLOPS, "traffic": None,
+               "mlp_arith_forward": args.arith,
+               "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": peaks[dominant],
+                            "unit": "TFLOP/s", "frac": ach / peaks[dominant], "traffic": None,
                             "kernels_ms": {k: v[1] for k, v in kern.items()},
-                            "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()}},
+                            "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()},
+                            "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()}},
                "stage_ms": stage_ms, "phase_ms": kt}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

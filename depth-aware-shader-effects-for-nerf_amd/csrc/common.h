@@ -62,7 +62,8 @@ int launch_ray_features(const float* packed, const float* dirs, int64_t R, const
                         int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
 extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
-                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s);
+                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
+                 float* save = nullptr, const float* encd = nullptr);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
                int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
                hipStream_t s, float* save = nullptr, const float* encd = nullptr);

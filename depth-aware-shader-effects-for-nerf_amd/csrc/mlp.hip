@@ -348,8 +348,8 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
                float* save, const float* encd) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
-  if (!save && g_mlp_arith == NERF_ARITH_F16X3)
-    return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s);
+  if (g_mlp_arith == NERF_ARITH_F16X3)
+    return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s, save, encd);
   constexpr int per_block = 32 * NERF_MLP_WAVES;
   const int64_t blocks = (M + per_block - 1) / per_block;
   if (save)

@@ -98,35 +98,12 @@ typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 // ---- the shared weight stream ------------------------------------------------------------
-// Chunk c (16 pieces of 1 KiB) into LDS slot SLOT; wave w moves pieces w, w+4, w+8, w+12.  Inline
-// asm in the saddr form (uniform 64-bit base in SGPRs + the lane's 32-bit offset `voff` =
-// 16*lane + 1024*wave, one VGPR for the whole kernel): the builtin's per-lane 64-bit addresses
-// cost 8 VGPRs per chunk.  hipcc counts none of these loads; the stream waits for them itself
-// (wait_vmcnt), and M0 is saved and restored around each.
-template <int SLOT>
-__device__ __forceinline__ void chunk_dma(const float* __restrict__ stream, int c, uint32_t lds_base, uint32_t voff) {
-  // lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece); voff: the
-  // lane's byte offset 16 * lane + 1024 * wave into the chunk
-#ifdef NERF16_T_NODMA
-  return;
-#endif
-  const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %2\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(src + i * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + i * (kW16Waves * 1024))
-        : "memory");
-  }
-}
-
-// Piece i (0..3) of this wave's share of chunk c into LDS slot SLOT.
+// Piece I (0..3) of this wave's share of chunk c into LDS slot SLOT: wave w moves pieces w, w+4,
+// w+8, w+12 of the chunk's 16 (1 KiB each).  Inline asm in the saddr form (uniform 64-bit base in
+// SGPRs + the lane's 32-bit offset `voff` = 16*lane + 1024*wave, one VGPR for the whole kernel):
+// the builtin's per-lane 64-bit addresses cost 8 VGPRs per chunk.  hipcc counts none of these
+// loads; the stream waits for them itself (wait_vmcnt), and M0 is saved and restored around each.
+// lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece).
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
                                                 uint32_t voff) {
@@ -146,11 +123,19 @@ __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream
       : "memory");
 }
 
+// This wave's whole share (4 pieces) of chunk c.
+template <int SLOT>
+__device__ __forceinline__ void chunk_dma(const float* __restrict__ stream, int c, uint32_t lds_base, uint32_t voff) {
+  chunk_dma_piece<SLOT, 0>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 1>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 2>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 3>(stream, c, lds_base, voff);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }   // lgkmcnt(0) only
 
 // A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
 template <int KK>
@@ -200,6 +185,13 @@ __device__ __forceinline__ constexpr int side_quarters(int hs) {
   if constexpr (KIND == kSideL0) return 4;
   return 0;
 }
+// Training forward (SAVE): global stores of ReLU(y) (one f32x4 per converted quarter) issued in
+// half-step hs; they count in vmcnt with the stream's DMA (skip-layer PE operands store nothing).
+template <int KIND>
+__device__ __forceinline__ constexpr int side_stores(int hs) {
+  if constexpr (KIND == kSideSkipPrev) return side_quarters<kSidePrev>(hs);
+  return side_quarters<KIND>(hs);
+}
 template <int KIND>
 __device__ __forceinline__ constexpr int side_vpg(int hs) {
   const int q = side_quarters<KIND>(hs);
@@ -220,13 +212,6 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
   mfma_kstep<G, FIRST>(am, b, acc, hook);
   side(std::integral_constant<int, 1>{});
-#ifdef NERF16_BUNCHED_SIDE   // the previous schedule: reads paired between tiles, VALU left to the compiler
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (READ) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
-    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                      // 3 MFMAs
-  }
-#else
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // 1 MFMA
@@ -237,7 +222,6 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
       if (i > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);         // VPG VALU (none in gap 0:
     }                                                                         // the bias reads land)
   }
-#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -247,32 +231,27 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
 //   the slot chunk c-1 used | MFMA k-step 1, reading chunk c+1's k-step-0 A
 // On entry chunk c is published, c+1 and c+2 are in flight and a0 holds k-step 0's fragments.
 // TAIL = chunks left after c, capped at 3: the stream's last steps stop loading and waiting.
-template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, typename Side0, typename Side1>
+template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, bool SV, typename Side0, typename Side1>
 __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int c, float* lds, uint32_t lds_dma,
                                            uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
                                            const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
                                            Side1&& side1) {
-#ifdef NERF16_EXPLICIT_LGKM
-  wait_lgkm0();                                     // a0's reads (interleaved in the last half-step) are in
-#endif
+  // (the fragment reads' lgkmcnt waits are the compiler's, per MFMA)
   half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
                                                     [](auto) {});
 #ifndef NERF16_T_NOBARRIER
+  // own DMA of chunk c+1 done: younger than it are chunk c+2's 4 pieces and, in the training
+  // forward, at least this half-step's stores (all issued after chunk c+1's pieces)
   if constexpr (TAIL >= 1) {
-    wait_vmcnt<TAIL >= 2 ? 4 : 0>();
+    wait_vmcnt<TAIL >= 2 ? 4 + (SV ? side_stores<KIND>(HS0) : 0) : 0>();
     __builtin_amdgcn_s_barrier();
   }
 #endif
-#ifdef NERF16_EXPLICIT_LGKM
-  wait_lgkm0();                                     // a1's reads are in
-#endif
-  // DMA of chunk c+3 into the slot chunk c-1 used: one piece after each tile's MFMAs
+  // DMA of chunk c+3 into the slot chunk c-1 used, one piece after each tile's MFMAs: inside the
+  // MFMA region (after the fragment reads, which the asm's memory clobber keeps ahead of it) the
+  // pieces cost 1.2K cycles per layer; issued as a block between the half-steps, 2.4K
   auto dma = [&](auto ti) __attribute__((always_inline)) {
-#ifdef NERF16_DMA_BUNCHED
-    if constexpr (TAIL >= 3 && decltype(ti)::value == 0) chunk_dma<(SLOT + 3) & 3>(stream, c + 3, lds_dma, voff);
-#else
     if constexpr (TAIL >= 3) chunk_dma_piece<(SLOT + 3) & 3, decltype(ti)::value>(stream, c + 3, lds_dma, voff);
-#endif
   };
   half_step<G, false, (TAIL >= 1), 0, side_vpg<KIND>(HS0 + 1)>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0,
                                                             lane, side1, dma);
@@ -281,15 +260,15 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
 // A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
 // the B operand of k-step 2i+kk; side(i, kk, phase) is the VALU work placed in that half-step:
 // phase 0 issues its LDS reads, phase 1 computes.
-// TAIL_END = chunks after this group (capped at 3).
-template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, typename Opnd, typename Side>
+// TAIL_END = chunks after this group (capped at 3); SV = the side work stores (training forward).
+template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, bool SV, typename Opnd, typename Side>
 __device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
                                           uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], f32x16 (&acc)[8],
                                           int lane, Opnd&& operand, Side&& side) {
   static_for<NSTEP>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     constexpr int left = NSTEP - 1 - i + TAIL_END;
-    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i>(
+    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i, SV>(
         stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
         operand(ic, std::integral_constant<int, 1>{}), acc, lane,
         [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}, ph); },
@@ -306,28 +285,44 @@ __device__ __forceinline__ void run_group(const float* __restrict__ stream, int 
 struct QuarterVec {
   f32x4 b, w;
 };
+struct SaveAt {      // training forward: where a layer's activations go (see convert4)
+  float* base;
+  uint32_t loff;
+  int hoff;
+  bool valid;
+};
 template <int T0, int QG, bool SIGMA>
 __device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
   qv.b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
   if constexpr (SIGMA) qv.w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
 }
-template <int T0, int OP0, int QG, bool SIGMA>
+// SV (training forward): also store ReLU(y) to the sample's activation row: `sv` = the wave's rows
+// (uniform base), lane offset `loff` = (lane & 31) * kSaveRow + 4h, layer slice `hoff` (uniform):
+// neuron 32T + 8q + 4h + e in the layout.h save order.  Uniform base + 32-bit lane offset keeps the
+// address in one VGPR.
+template <int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const QuarterVec& qv, float s,
-                                         Operand (&in)[16], float& m, float& part) {
+                                         Operand (&in)[16], float& m, float& part, const SaveAt& sv) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
+  f32x4 rv;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, qv.b[e]), 0.0f);
+    rv[e] = r;
     m = fmaxf(m, r);
     if constexpr (SIGMA) part = fmaf(qv.w[e], r, part);
     split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
   }
+  if constexpr (SV) {
+    if (sv.valid) *reinterpret_cast<f32x4*>(sv.base + (sv.loff + (uint32_t)(sv.hoff + 32 * T + 8 * q))) = rv;
+  }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
-template <int PH, int T0, int OP0, int QG, bool SIGMA>
+template <int PH, int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const float* bias, const float* ws, int h,
-                                        float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv) {
+                                        float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv,
+                                        const SaveAt& sv) {
 #ifdef NERF16_T_NOSIDE   // timing-only builds: no epilogue conversions (one register kept live); wrong results
   if constexpr (PH == 1) {
     constexpr int T = T0 + QG / 4, q = QG % 4;
@@ -336,7 +331,7 @@ __device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const
   return;
 #endif
   if constexpr (PH == 0) load4<T0, QG, SIGMA>(bias, ws, h, qv);
-  else convert4<T0, OP0, QG, SIGMA>(acc, inv, qv, s, in, m, part);
+  else convert4<T0, OP0, QG, SIGMA, SV>(acc, inv, qv, s, in, m, part, sv);
 }
 
 // PE operand Q split at scale s from this wave's LDS copy (layer 4 reads [h3, enc_x]): phase 0
@@ -363,10 +358,15 @@ struct NoSide {
 template <typename I, typename K>
 __device__ __forceinline__ constexpr int kstep_of(I, K) { return 2 * I::value + K::value; }
 
+// SAVE = the training forward (nerf_mlp_forward_train): also writes each sample's activation row
+// (layout.h kSave*: h_0..h_7 from the epilogue quarters, enc_x, enc_d, r_dir, hd from the heads)
+// to `save` (M x kSaveRow); encd (R x 32) holds each ray's PE_4(d) from nerf_ray_features.
+template <bool SAVE>
 __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
              const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
-             float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T) {
+             float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
+             float* __restrict__ save, const float* __restrict__ encd) {
   __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
   STAMP16(0);
@@ -375,6 +375,9 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   const bool valid = s0 + (lane & 31) < M;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const int64_t r = s / N;
+  // training: the wave's activation rows (uniform) and this lane's offset into them
+  float* const wrow = SAVE ? save + s0 * kSaveRow : nullptr;
+  const uint32_t loff = (uint32_t)(lane & 31) * kSaveRow + 4 * h;
 
   // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
   float x[3];
@@ -456,20 +459,22 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   // ---- layer 0: PE(63) -> 256, 2 chunk-steps per group ----
   auto pe_operand_of = [&](auto i, auto kk) -> const Operand& { return pe_op[kstep_of(i, kk)]; };
-  run_group<0, 2, 0, 3, kSideNone>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
+  run_group<0, 2, 0, 3, kSideNone, SAVE>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
   // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE),
   // 4 quarters per half-step
   QuarterVec qv[4];
   float pe_v[8];
-  run_group<1, 2, 2, 3, kSideL0>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
-                                 [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
-                                   constexpr int hs = kstep_of(i, kk);
-                                   static_for<4>([&](auto qc) __attribute__((always_inline)) {
-                                     constexpr int j = decltype(qc)::value;
-                                     quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false>(
-                                         acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j]);
-                                   });
-                                 });
+  SaveAt sv_prev{wrow, loff, save_h(0), valid};   // training: save slices of y_{L-1}, y_L
+  SaveAt sv_cur = sv_prev;
+  run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
+                                       [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                         constexpr int hs = kstep_of(i, kk);
+                                         static_for<4>([&](auto qc) __attribute__((always_inline)) {
+                                           constexpr int j = decltype(qc)::value;
+                                           quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false, SAVE>(
+                                               acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j], sv_cur);
+                                         });
+                                       });
   STAMP16(2);
 
   // ---- layers 1..7 ----
@@ -498,10 +503,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs == 0) {
-      quarter<P, 4, 8, 0, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0]);
-      quarter<P, 4, 8, 1, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1]);
+      quarter<P, 4, 8, 0, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
+      quarter<P, 4, 8, 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1], sv_prev);
     } else if constexpr (hs <= 14) {
-      quarter<P, 4, 8, hs + 1, sg>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0]);
+      quarter<P, 4, 8, hs + 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
     }
   };
   // group B's side: this layer's y_L tiles 0-3
@@ -509,10 +514,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs >= 1 && hs <= 14) {
-      quarter<P, 0, 0, hs - 1, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0]);
+      quarter<P, 0, 0, hs - 1, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
     } else if constexpr (hs == 15) {
-      quarter<P, 0, 0, 14, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0]);
-      quarter<P, 0, 0, 15, sg>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1]);
+      quarter<P, 0, 0, 14, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
+      quarter<P, 0, 0, 15, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1], sv_cur);
     }
   };
   using NoSigma = std::false_type;
@@ -522,11 +527,15 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     inv_cur = cst[kS16InvW + L] / s_cur;
     const float* bias_l = bias + L * kHidden;
     const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
+    if constexpr (SAVE) {
+      sv_prev.hoff = save_h(L - 1);
+      sv_cur.hoff = save_h(L);
+    }
     // group A (k-steps 0..15, + PE 16..19 at layer 4)
     if (L == kSkipLayer) {
       // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
       // read at hs 16 + q)
-      run_group<0, 10, 0, 3, kSideSkipPrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+      run_group<0, 10, 0, 3, kSideSkipPrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
                                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
                                               constexpr int hs = kstep_of(i, kk);
                                               side_prev(i, kk, ph, NoSigma{});
@@ -535,7 +544,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
                                                                                          pe_v, lane);
                                             });
     } else {
-      run_group<0, 8, 0, 3, kSidePrev>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<0, 8, 0, 3, kSidePrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, NoSigma{}); });
     }
     // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
@@ -546,13 +555,13 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     m = 0.0f;
     // group B (layer 7 also starts the density head)
     if (L == kSkipLayer) {
-      run_group<1, 10, 2, 3, kSideCur>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+      run_group<1, 10, 2, 3, kSideCur, SAVE>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
     } else if (L == 7) {
-      run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, Sigma{}); });
     } else {
-      run_group<1, 8, 0, 3, kSideCur>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+      run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
     }
     inv_prev = inv_cur;
@@ -583,7 +592,8 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
         : "memory");
   }
   inv_cur = cst[kS16InvW + 8] / s_cur;
-  run_group<0, 8, 0, 0, kSidePrev>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+  if constexpr (SAVE) sv_prev.hoff = save_h(7);
+  run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
   STAMP16(10);
 
@@ -600,9 +610,18 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
       for (int q = 0; q < 4; ++q) {
         const f32x4 fd = *reinterpret_cast<const f32x4*>(fr + t * 32 + 8 * q + 4 * h);
         const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
-        float hd[4];
+        f32x4 rd, hd;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) hd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f) + ap[e];
+        for (int e = 0; e < 4; ++e) {
+          rd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f);
+          hd[e] = rd[e] + ap[e];
+        }
+        if constexpr (SAVE) {
+          if (valid) {
+            *reinterpret_cast<f32x4*>(wrow + (loff + (uint32_t)(kSaveRDir + t * 32 + 8 * q))) = rd;
+            *reinterpret_cast<f32x4*>(wrow + (loff + (uint32_t)(kSaveHd + t * 32 + 8 * q))) = hd;
+          }
+        }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
@@ -623,6 +642,19 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
     out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
   }
+  if constexpr (SAVE) {
+    if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d
+#pragma unroll
+      for (int p = 0; p < kPeSteps; ++p) {
+        const int f = pe_feature(p, h);
+        wrow[loff - 4 * h + (uint32_t)(kSaveEncX + (f < 0 ? kPosEnc : f))] = f < 0 ? 0.0f : pe_mine[p * 64 + lane];
+      }
+      const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(wrow + (loff + 12 * h + (uint32_t)(kSaveEncD + 4 * q))) = ed[q];
+    }
+  }
   if (h == 0 && valid) {
     const int64_t o_s = out_slot ? r * out_T + slot : s;
     sigma[o_s] = sig;
@@ -633,13 +665,18 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 }
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
-                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s) {
+                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
+                 float* save, const float* encd) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   constexpr int per_block = 32 * kW16Waves;
   const int64_t blocks = (M + per_block - 1) / per_block;
-  hipLaunchKernelGGL(mlp16_kernel, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N, feat,
-                     rgb, sigma, out_slot, out_T);
+  if (save)
+    hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
+                       feat, rgb, sigma, out_slot, out_T, save, encd);
+  else
+    hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
+                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr);
   return check_launch("mlp16_kernel");
 }
 

@@ -34,16 +34,28 @@ int main() {
   (void)hipMalloc(&z, M * 4); (void)hipMemcpy(z, zz.data(), M * 4, hipMemcpyHostToDevice);
   (void)hipMalloc(&feat, R * 256 * 4); (void)hipMemset(feat, 0, R * 256 * 4);
   (void)hipMalloc(&rgb, M * 12); (void)hipMalloc(&sig, M * 4);
-  hipEvent_t e0, e1;
-  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-  for (int rep = 0; rep < 2; ++rep) {
-    (void)hipEventRecord(e0, 0);
+  // STAMP_REPS back-to-back launches (default 2): the last one is stamped and timed; with more
+  // reps the per-launch times show the clock the chip settles at under sustained load.
+  const int reps = getenv("STAMP_REPS") ? atoi(getenv("STAMP_REPS")) : 2;
+  std::vector<hipEvent_t> ev(reps + 1);
+  for (auto& e : ev) (void)hipEventCreate(&e);
+  (void)hipEventRecord(ev[0], 0);
+  for (int rep = 0; rep < reps; ++rep) {
     nerf::launch_mlp16(packed, o, d, z, R, N, feat, rgb, sig, nullptr, 0, 0);
-    (void)hipEventRecord(e1, 0);
+    (void)hipEventRecord(ev[rep + 1], 0);
   }
   (void)hipDeviceSynchronize();
   float ms = 0;
-  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventElapsedTime(&ms, ev[reps - 1], ev[reps]);
+  if (reps > 2) {
+    printf("per-launch ms:");
+    for (int rep = 0; rep < reps; ++rep) {
+      float t = 0;
+      (void)hipEventElapsedTime(&t, ev[rep], ev[rep + 1]);
+      printf(" %.1f", t);
+    }
+    printf("\n");
+  }
   static unsigned long long st[65536][16];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(nerf::nerf16_stamps), sizeof(st));
   struct Seg { const char* name; int a, b; };

@@ -20,6 +20,16 @@ from oracle import nerf_oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True, params=["f16x3", "f32"])
+def arith(request):
+    """The training forward runs on the MLP arithmetic in force (include/nerfmi.h, nerf_arith):
+    every test here runs under both."""
+    from nerfmi import _lib as L
+    prev = L.set_mlp_arith(request.param)
+    yield request.param
+    L.set_mlp_arith(prev)
+
+
 def _lib():
     from nerfmi import _lib as L
     return L
@@ -127,9 +137,10 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
                 dexp=dexp, rgb_o=rgb_o.detach(), sigma_o=sigma_o.detach(), pres=pres, st64=st64)
 
 
-@pytest.mark.parametrize("with_app", [False, True])
-def test_forward_saves_are_the_activations(ref_state, app_vec, with_app):
-    r = _mlp_forward_backward(ref_state, app_vec if with_app else None)
+@pytest.mark.parametrize("with_app,N", [(False, 11), (True, 11), (True, 64)])
+def test_forward_saves_are_the_activations(ref_state, app_vec, with_app, N):
+    """N = 64: a wave's 32 samples share one ray (the f16x3 kernel's LDS feature path)."""
+    r = _mlp_forward_backward(ref_state, app_vec if with_app else None, R=40 if N == 64 else 96, N=N)
     np.testing.assert_allclose(r["rgb"].numpy(), r["rgb_o"].numpy(), rtol=1e-4, atol=1e-6)
     save = r["save"].numpy()
     offs = [0, 256, 512, 768, 1088, 1344, 1600, 1856]
@@ -242,12 +253,20 @@ def _trainer(ref_state, n_images=100):
     return Trainer(nerfmi.Config(), model=model, appearance_embeddings=table), table
 
 
-def _params_close(got, exp, steps, name, frac=0.999, lr=5e-4):
+def _params_close(got, exp, steps, name, frac=0.999, lr=5e-4, rel_g=None, rel_g_max=1e-3):
     """Adam normalises each gradient entry by its own RMS, so an entry whose true gradient is ~0
     (cancellation) moves by up to lr per step in whichever direction its rounding points: require
-    almost all entries within 2e-6 and every entry within the 2*lr*steps such a flip can cause."""
+    almost all entries within 2e-6 and every entry within the 2*lr*steps such a flip can cause.
+    With rel_g (per entry, the reference gradient's magnitude over the tensor's largest, the
+    smallest over the steps), each entry off by more than 2e-6 must also be one whose reference
+    gradient was ~0 (rel_g <= rel_g_max) at some step; frac=None drops the fraction test."""
     d = np.abs(np.asarray(got, np.float64) - np.asarray(exp, np.float64))
-    assert (d <= 2e-6).mean() >= frac, (name, (d <= 2e-6).mean())
+    if frac is not None:
+        assert (d <= 2e-6).mean() >= frac, (name, (d <= 2e-6).mean())
+    if rel_g is not None:
+        off = d > 2e-6
+        r = np.asarray(rel_g, np.float64).reshape(d.shape)
+        assert np.all(r[off] <= rel_g_max), (name, int(off.sum()), float(r[off].max()))
     assert d.max() <= 2 * lr * steps + 2e-6, (name, d.max())
 
 
@@ -278,7 +297,8 @@ def test_trainer_step_matches_reference_f7(golden, golden_meta, ref_state):
             _params_close(prm.reshape(-1)[idx].numpy(), f7[f"param/{name}"], 1, name, frac=0.95)
         else:
             assert rel_l2(g.numpy(), f7[f"grad/{name}"]) < 5e-4, name
-            _params_close(prm.numpy(), f7[f"param/{name}"], 1, name)
+            ga = np.abs(f7[f"grad/{name}"].astype(np.float64))
+            _params_close(prm.numpy(), f7[f"param/{name}"], 1, name, frac=None, rel_g=ga / max(ga.max(), 1e-30))
 
 
 def test_trainer_matches_oracle_over_steps(ref_state):
@@ -313,7 +333,10 @@ def test_trainer_matches_oracle_over_steps(ref_state):
     for i, n in enumerate(names):
         got = tr.view(tr.flat, i).detach().cpu().numpy()
         exp = params[n].detach().numpy()
-        _params_close(got, exp, 3, n, frac=0.99)
+        # after 3 steps a sign flip at one step feeds the later steps' gradients, so which entries
+        # differ is no longer local (the one-step F7 test checks the flip criterion entry by
+        # entry): up to 2% of entries may differ, each within the 2*lr*steps bound
+        _params_close(got, exp, 3, n, frac=0.98)
 
 
 def test_training_reduces_loss_on_teacher_scene():
