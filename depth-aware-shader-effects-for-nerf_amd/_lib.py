@@ -82,10 +82,17 @@ _SIGNATURES = {
                                           _V]),
     "nerf_train_backward": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _I64,
                                            ctypes.POINTER(ctypes.c_void_p), _V, _V, _V, ctypes.c_size_t, _V]),
+    # depth-aware post effects (include/nerfmi.h)
+    "nerf_effect_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "nerf_depth_normalize": (ctypes.c_int, [_V, _I64, _V, _V, ctypes.c_size_t, _V]),
+    "nerf_effect_fog": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V, _V,
+                                       ctypes.c_size_t, _V]),
+    "nerf_effect_toon": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V,
+                                        _V, ctypes.c_size_t, _V]),
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

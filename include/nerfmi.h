@@ -166,6 +166,27 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
                      float* coarse_depth, void* workspace, size_t ws_bytes,
                      nerf_stream_t stream);
 
+/* ------------------------------------------------- depth-aware post effects
+ * The depth-reading effects of the reference's PostProcessor (src/post_processor.py) on the
+ * frame run.py renders.  image / out: uint8 (H,W,3) RGB; depth: fp32 (H,W)
+ * or the first channel of (H,W,C) with depth_stride = C, nullable (each effect's no-depth
+ * branch).  workspace: nerf_effect_workspace_bytes(H, W) device bytes.
+ *   nerf_depth_normalize   run.py:248: (d - min) / (max - min + 1e-6) over n values.
+ *   nerf_effect_fog        Fog (post_processor.py:451-493): white fog, fog_start < 1.
+ *   nerf_effect_toon       Toon Shader (post_processor.py:64-117): colours quantised to `levels`,
+ *                          depth edges (bilateral 9/75/75, Sobel, threshold 0.05, 3x3 dilation) or,
+ *                          without depth, colour edges (gray Laplacian, threshold 0.1) darkened by
+ *                          edge_strength.  The cv2 steps are OpenCV 4's algorithms restated. */
+size_t nerf_effect_workspace_bytes(int H, int W);
+int nerf_depth_normalize(const float* depth, int64_t n, float* out, void* workspace, size_t ws_bytes,
+                         nerf_stream_t stream);
+int nerf_effect_fog(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W,
+                    double fog_start, uint8_t* out, void* workspace, size_t ws_bytes,
+                    nerf_stream_t stream);
+int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W,
+                     int levels, double edge_strength, uint8_t* out, void* workspace,
+                     size_t ws_bytes, nerf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,8 +13,15 @@ Added flags: --random_init SEED renders a seeded random-init model when no check
 ignores n_importance, render.py:83-86) with --n_importance samples; --chunk renders the frame
 in ray chunks (0 = whole frame per call).  Under torchrun every frame is ray-sharded across
 the ranks (frames.py) and rank 0 writes the images.
-Out of scope here: training (--mode train), post-processing shaders
-(--use_shader) and video encoding (--mode video, --create_video; cv2 is absent).
+--mode train runs the reference's training loop (run.py:326-347 -> src/train.py) on the nerfmi
+kernels (nerfmi.train.train_nerf; the nerf_synthetic scene when present, else the
+teacher-rendered synthetic scene), data-parallel under torchrun; --iterations overrides
+Config.num_iterations.  --use_shader / --shader NAME applies a depth-aware effect of the
+reference's PostProcessor on the GPU (nerfmi.PostProcessor: "Fog", "Toon Shader", "Original") to
+each frame before it is written, with run.py:248's depth normalisation; the reference's
+interactive first-frame editor (tkinter) is not reproduced, so --shader names the effect
+(default with --use_shader alone: Fog).  Out of scope: video encoding (--mode
+video, --create_video; cv2 is absent).
 Camera metadata: data/nerf_synthetic/<scene>/transforms_test.json when present (focal from
 camera_angle_x, dataset.py:66); otherwise the public nerf_synthetic value at 800x800.
 """
@@ -61,6 +68,7 @@ def parse_args(argv=None):
     p.add_argument('--n_importance', type=int, default=None, help='fine samples (default Config.num_importance)')
     p.add_argument('--chunk', type=int, default=0, help='rays per render call (0 = whole frame)')
     p.add_argument('--seed', type=int, default=0, help='seed of the in-kernel sampling RNG')
+    p.add_argument('--iterations', type=int, default=None, help='training iterations (default Config)')
     return p.parse_args(argv)
 
 
@@ -93,7 +101,7 @@ class SceneInfo:
 def render_path(model, scene, config, output_dir, num_frames=120, quality='high', width=800, height=800,
                 start_frame=0, end_frame=None, save_depth=False, raw_output=False, camera_path='circle',
                 spiral_loops=2.0, height_range=(-0.5, 0.5), hierarchical=False, n_importance=None, chunk=0,
-                seed=0):
+                seed=0, shader=None):
     """run.py:63-282 (render mode) on nerfmi."""
     import torch.distributed as dist
     from nerfmi import cameras, frames
@@ -134,13 +142,14 @@ def render_path(model, scene, config, output_dir, num_frames=120, quality='high'
             depth = torch.cat([dd for _, dd in outs]).reshape(height, width).cpu()
         if rank != 0:
             continue
-        write_frame(output_dir, frame_idx, rgb, depth, save_depth, raw_output)
+        write_frame(output_dir, frame_idx, rgb, depth, save_depth, raw_output, shader)
     if rank == 0:
         print(f"Rendered {len(theta)} frames to {output_dir}")
 
 
-def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=False):
-    """Outputs of run.py:233-275."""
+def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=False, shader=None):
+    """Outputs of run.py:233-275; with `shader`, the effect is applied to the written rgb image
+    (not the raw one) after run.py:248's depth normalisation, both on the GPU."""
     from PIL import Image
     rgb_img = (rgb * 255).numpy().astype(np.uint8)            # truncation, run.py:233
     depth_img = depth.numpy()
@@ -151,6 +160,11 @@ def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=
         Image.fromarray(rgb_img).save(os.path.join(raw_dir, f'rgb_{frame_idx:03d}.png'))
     if save_depth:
         np.save(os.path.join(raw_dir, f'depth_{frame_idx:03d}.npy'), depth_img)
+    if shader and not raw_output:                             # run.py:247-262
+        from nerfmi.post_processor import PostProcessor, normalize_depth
+        processor = PostProcessor()
+        processor.current_effect = shader
+        rgb_img = processor.apply_effect(rgb_img, normalize_depth(depth_img))
     Image.fromarray(rgb_img).save(os.path.join(output_dir, f'rgb_{frame_idx:03d}.png'))
     import matplotlib
     matplotlib.use('Agg')
@@ -168,21 +182,33 @@ def main(argv=None):
     import nerfmi
     config = nerfmi.Config()
     config.scene = args.scene
-    if args.mode == 'train':
-        print("nerfmi: training is not part of this build yet (SURVEY.md §8f row 2); use --mode render")
-        return 2
     if args.mode == 'video' or args.create_video:
         print("nerfmi: video encoding is out of scope (post-processing, SURVEY.md §2; cv2 is absent)")
         if args.mode == 'video':
             return 2
-    if args.use_shader or args.shader:
-        print("nerfmi: depth-aware shader effects are out of scope (SURVEY.md §2); writing raw renders")
+    shader = args.shader or ('Fog' if args.use_shader else None)
+    if shader:
+        from nerfmi.post_processor import PostProcessor
+        if shader not in PostProcessor().effects:
+            print(f"nerfmi: effect {shader!r} is not on the GPU path; available: {sorted(PostProcessor().effects)}")
+            return 2
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1:
         local = int(os.environ.get('LOCAL_RANK', '0'))
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    if args.mode == 'train':                                           # run.py:326-347
+        from nerfmi.dataset import make_dataset
+        from nerfmi.train import train_nerf
+        np.random.seed(args.seed + (dist.get_rank() if world > 1 else 0))
+        dataset = make_dataset(config)
+        torch.manual_seed(args.random_init or 0)
+        train_nerf(config, dataset, save_dir=f"checkpoints_{args.scene}", num_iterations=args.iterations,
+                   group=dist.group.WORLD if world > 1 else None)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
     checkpoint = args.checkpoint
     if not checkpoint and args.random_init is None:
         default = f"checkpoints_{args.scene}/checkpoint_final.pt"     # run.py:351-359
@@ -208,7 +234,7 @@ def main(argv=None):
                     save_depth=args.save_depth, raw_output=args.raw_output, camera_path=args.camera_path,
                     spiral_loops=args.spiral_loops, height_range=args.height_range,
                     hierarchical=args.hierarchical, n_importance=args.n_importance, chunk=args.chunk,
-                    seed=args.seed)
+                    seed=args.seed, shader=shader)
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -58,8 +58,41 @@ def test_write_frame_outputs(tmp_path):
 
 
 def test_out_of_scope_modes_say_so(capsys):
-    assert cli.main(["--mode", "train"]) == 2
-    assert "training" in capsys.readouterr().out
+    assert cli.main(["--mode", "video"]) == 2
+    assert "video" in capsys.readouterr().out
+
+
+@pytest.mark.gpu
+def test_unknown_shader_is_refused(capsys):
+    assert cli.main(["--mode", "render", "--random_init", "0", "--shader", "Sepia"]) == 2
+    assert "Sepia" in capsys.readouterr().out
+
+
+@pytest.mark.gpu
+def test_render_with_shader_applies_the_effect(tmp_path):
+    """--shader Fog writes the GPU Fog of the plain frame, with run.py:248's depth normalisation."""
+    from PIL import Image
+    from nerfmi.post_processor import PostProcessor, normalize_depth
+    base = ["--mode", "render", "--scene", "chair", "--random_init", "0", "--frames", "1", "--width", "40",
+            "--height", "24", "--quality", "preview", "--save_depth"]
+    plain, fog = str(tmp_path / "plain"), str(tmp_path / "fog")
+    assert cli.main(base + ["--output_dir", plain]) == 0
+    assert cli.main(base + ["--output_dir", fog, "--shader", "Fog"]) == 0
+    img = np.array(Image.open(os.path.join(plain, "rgb_000.png")))
+    depth = np.load(os.path.join(plain, "raw", "depth_000.npy"))
+    pp = PostProcessor()
+    pp.current_effect = "Fog"
+    exp = pp.apply_effect(img, normalize_depth(depth))
+    assert np.array_equal(np.array(Image.open(os.path.join(fog, "rgb_000.png"))), exp)
+
+
+@pytest.mark.gpu
+def test_train_mode_runs_the_training_loop(tmp_path, monkeypatch):
+    """--mode train (run.py:326-347) on the synthetic scene: a few iterations, a final checkpoint."""
+    monkeypatch.chdir(tmp_path)
+    assert cli.main(["--mode", "train", "--scene", "chair", "--iterations", "3", "--random_init", "0"]) == 0
+    files = os.listdir(tmp_path / "checkpoints_chair")
+    assert any(f.endswith(".pt") for f in files), files
 
 
 @pytest.mark.gpu
