@@ -285,22 +285,26 @@ __device__ __forceinline__ void run_group(const float* __restrict__ stream, int 
 struct QuarterVec {
   f32x4 b, w;
 };
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 struct SaveAt {      // training forward: where a layer's activations go (see convert4)
-  float* base;
-  uint32_t loff;
-  int hoff;
+  __amdgpu_buffer_rsrc_t rows;   // the wave's 32 activation rows
+  uint32_t loff;                 // this lane's byte offset in them: ((lane & 31) * kSaveRow + 4h) * 4
+  int hoff;                      // the layer's slice (floats), uniform
   bool valid;
 };
+// 16 bytes at byte offset voff + 4 * (hoff + c) of the wave's rows: a buffer store, so the lane's
+// address stays one VGPR (the uniform slice goes in soffset, the constant in the offset field).
+__device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sv.rows, (int)sv.loff + 4 * c, 4 * sv.hoff, 0);
+}
 template <int T0, int QG, bool SIGMA>
 __device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
   qv.b = *reinterpret_cast<const f32x4*>(bias + 32 * T + 8 * q + 4 * h);
   if constexpr (SIGMA) qv.w = *reinterpret_cast<const f32x4*>(ws + 32 * T + 8 * q + 4 * h);
 }
-// SV (training forward): also store ReLU(y) to the sample's activation row: `sv` = the wave's rows
-// (uniform base), lane offset `loff` = (lane & 31) * kSaveRow + 4h, layer slice `hoff` (uniform):
-// neuron 32T + 8q + 4h + e in the layout.h save order.  Uniform base + 32-bit lane offset keeps the
-// address in one VGPR.
+// SV (training forward): also store ReLU(y) to the sample's activation row (SaveAt): neuron
+// 32T + 8q + 4h + e of the layer's slice, the layout.h save order.
 template <int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const QuarterVec& qv, float s,
                                          Operand (&in)[16], float& m, float& part, const SaveAt& sv) {
@@ -315,7 +319,7 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
   }
   if constexpr (SV) {
-    if (sv.valid) *reinterpret_cast<f32x4*>(sv.base + (sv.loff + (uint32_t)(sv.hoff + 32 * T + 8 * q))) = rv;
+    save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
   }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
@@ -376,8 +380,12 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const int64_t r = s / N;
   // training: the wave's activation rows (uniform) and this lane's offset into them
-  float* const wrow = SAVE ? save + s0 * kSaveRow : nullptr;
-  const uint32_t loff = (uint32_t)(lane & 31) * kSaveRow + 4 * h;
+  __amdgpu_buffer_rsrc_t wrows;
+  if constexpr (SAVE)
+    wrows = __builtin_amdgcn_make_buffer_rsrc(save + s0 * kSaveRow, (short)0, 32 * kSaveRow * 4, 0x00020000);
+  // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
+  // inside the MFMA schedule)
+  const uint32_t loff = valid ? ((uint32_t)(lane & 31) * kSaveRow + 4 * h) * 4 : 0x40000000u;
 
   // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
   float x[3];
@@ -464,7 +472,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // 4 quarters per half-step
   QuarterVec qv[4];
   float pe_v[8];
-  SaveAt sv_prev{wrow, loff, save_h(0), valid};   // training: save slices of y_{L-1}, y_L
+  SaveAt sv_prev{wrows, loff, save_h(0), valid};   // training: save slices of y_{L-1}, y_L
   SaveAt sv_cur = sv_prev;
   run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
                                        [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
@@ -617,10 +625,9 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
           hd[e] = rd[e] + ap[e];
         }
         if constexpr (SAVE) {
-          if (valid) {
-            *reinterpret_cast<f32x4*>(wrow + (loff + (uint32_t)(kSaveRDir + t * 32 + 8 * q))) = rd;
-            *reinterpret_cast<f32x4*>(wrow + (loff + (uint32_t)(kSaveHd + t * 32 + 8 * q))) = hd;
-          }
+          const SaveAt at{wrows, loff, 0, true};
+          save_store(at, kSaveRDir + t * 32 + 8 * q, rd);
+          save_store(at, kSaveHd + t * 32 + 8 * q, hd);
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -647,12 +654,13 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
       for (int p = 0; p < kPeSteps; ++p) {
         const int f = pe_feature(p, h);
-        wrow[loff - 4 * h + (uint32_t)(kSaveEncX + (f < 0 ? kPosEnc : f))] = f < 0 ? 0.0f : pe_mine[p * 64 + lane];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? 0.0f : pe_mine[p * 64 + lane]), wrows,
+                                              (int)loff - 16 * h + 4 * (kSaveEncX + (f < 0 ? kPosEnc : f)), 0, 0);
       }
       const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<f32x4*>(wrow + (loff + 12 * h + (uint32_t)(kSaveEncD + 4 * q))) = ed[q];
+        save_store(SaveAt{wrows, loff, 0, true}, 12 * h + kSaveEncD + 4 * q, ed[q]);
     }
   }
   if (h == 0 && valid) {
