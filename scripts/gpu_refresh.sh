@@ -9,4 +9,4 @@ python scripts/summarize_pmc.py gpurun_out/pmc16 gpurun_out/pmc16_summary.json |
 scripts/gpu_check.sh bench || exit $?
 cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_f16 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_f16.log 2>&1 || exit $?
-scripts/gpu_check.sh bench_train
+scripts/gpu_check.sh bench_train bench_f32

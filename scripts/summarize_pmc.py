@@ -12,6 +12,9 @@ dur = collections.defaultdict(dict)
 for f in sorted(glob.glob(os.path.join(src, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
+        if k.startswith("void "):
+            k = k[5:]
+        k = k.split("<")[0]            # template instances (nerf::mlp16_kernel<false>) under one name
         per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[k][(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
 res = {"source": src, "kernels": {}}
