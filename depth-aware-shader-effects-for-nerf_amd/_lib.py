@@ -10,7 +10,8 @@ import os
 import torch
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG_DIR, "libnerfmi.so")
+# NERFMI_LIB: an alternative build of the same library (A/B timing of kernel variants on one box)
+LIB_PATH = os.environ.get("NERFMI_LIB") or os.path.join(_PKG_DIR, "libnerfmi.so")
 
 _c_float_p = ctypes.c_void_p  # device pointers travel as integers
 _V, _I64 = ctypes.c_void_p, ctypes.c_int64

@@ -102,7 +102,9 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // w+8, w+12 of the chunk's 16 (1 KiB each).  Inline asm in the saddr form (uniform 64-bit base in
 // SGPRs + the lane's 32-bit offset `voff` = 16*lane + 1024*wave, one VGPR for the whole kernel):
 // the builtin's per-lane 64-bit addresses cost 8 VGPRs per chunk.  hipcc counts none of these
-// loads; the stream waits for them itself (wait_vmcnt), and M0 is saved and restored around each.
+// loads; the stream waits for them itself (wait_vmcnt).  M0 is declared clobbered rather than
+// saved and restored (nothing else in the kernel uses it): -2 SALU per piece, 144K -> 140K cycles
+// per wave, +0.8 % frame rate in a same-box A/B (scripts/ab_bench.sh).
 // lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece).
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
@@ -111,6 +113,7 @@ __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream
   return;
 #endif
   const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
+#ifdef NERF16_M0_SAVE
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -121,6 +124,15 @@ __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream
       : "=&s"(keep)
       : "v"(voff), "s"(src + I * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + I * (kW16Waves * 1024))
       : "memory");
+#else
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, %1"
+      :
+      : "v"(voff), "s"(src + I * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + I * (kW16Waves * 1024))
+      : "memory", "m0");
+#endif
 }
 
 // This wave's whole share (4 pieces) of chunk c.
