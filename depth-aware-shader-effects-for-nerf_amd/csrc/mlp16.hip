@@ -207,7 +207,10 @@ __device__ __forceinline__ constexpr int side_stores(int hs) {
 template <int KIND>
 __device__ __forceinline__ constexpr int side_vpg(int hs) {
   const int q = side_quarters<KIND>(hs);
-  return q == 0 ? 0 : (q * 40 + 10) / 11;
+#ifndef NERF16_VALU_PER_QUARTER
+#define NERF16_VALU_PER_QUARTER 40
+#endif
+  return q == 0 ? 0 : (q * NERF16_VALU_PER_QUARTER + 10) / 11;
 }
 
 // Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
@@ -224,15 +227,25 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
   mfma_kstep<G, FIRST>(am, b, acc, hook);
   side(std::integral_constant<int, 1>{});
+#ifndef NERF16_DSR_PER_GAP
+#define NERF16_DSR_PER_GAP 1
+#endif
+#ifndef NERF16_DSR_GAP0
+#define NERF16_DSR_GAP0 2
+#endif
+#ifndef NERF16_VALU_GAP0
+#define NERF16_VALU_GAP0 1
+#endif
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // 1 MFMA
     if constexpr (READ) {
-      if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         // 1 DS read
+      if (i >= NERF16_DSR_GAP0 && i < NERF16_DSR_GAP0 + 8 / NERF16_DSR_PER_GAP)
+        __builtin_amdgcn_sched_group_barrier(0x100, NERF16_DSR_PER_GAP, 0);   // DS reads
     }
     if constexpr (VPG > 0) {
-      if (i > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);         // VPG VALU (none in gap 0:
-    }                                                                         // the bias reads land)
+      if (i >= NERF16_VALU_GAP0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VPG VALU (none in
+    }                                                                                   // gap 0: bias reads land)
   }
   __builtin_amdgcn_sched_barrier(0);
 }
