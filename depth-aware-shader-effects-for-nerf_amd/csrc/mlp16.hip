@@ -103,8 +103,11 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // SGPRs + the lane's 32-bit offset `voff` = 16*lane + 1024*wave, one VGPR for the whole kernel):
 // the builtin's per-lane 64-bit addresses cost 8 VGPRs per chunk.  hipcc counts none of these
 // loads; the stream waits for them itself (wait_vmcnt).  M0 is declared clobbered rather than
-// saved and restored (nothing else in the kernel uses it): -2 SALU per piece, 144K -> 140K cycles
-// per wave, +0.8 % frame rate in a same-box A/B (scripts/ab_bench.sh).
+// saved and restored: -2 SALU per piece, 144K -> 140K cycles per wave, +0.8 % frame rate in a
+// same-box A/B (scripts/ab_bench.sh).  hipcc warns that it does not preserve M0 across such an
+// asm; that is safe only while nothing else in the kernel reads M0 (no LDS-DMA builtin, s_movrel,
+// ds_*_addtid or GWS): the generated code's only M0 writes are these (checked in the .s; the
+// Makefile silences the warning for this file).
 // lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece).
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
