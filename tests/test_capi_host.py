@@ -56,6 +56,17 @@ def test_bad_arguments_are_reported_not_launched():
     assert ws == 3 * 256 * 257 * 4                      # 2048-sample chunks x N x (K + bias column)
     assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2312) * 4
     assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, 0, None, None) == 0
+    # post effects
+    assert lib.nerf_effect_workspace_bytes(0, 8) == 0
+    assert lib.nerf_effect_workspace_bytes(800, 800) >= 256 + 2 * 800 * 800 * 4
+    rc = lib.nerf_effect_fog(None, None, 1, 8, 8, 0.1, None, None, 0, None)
+    assert rc == 1 and b"nerf_effect_fog" in lib.nerf_last_error()
+    rc = lib.nerf_effect_fog(None, None, 0, 8, 8, 0.1, None, None, 0, None)      # depth stride < 1
+    assert rc == 1
+    rc = lib.nerf_effect_toon(None, None, 1, 8, 8, 0, 1.0, None, None, 0, None)   # levels must be > 0
+    assert rc == 1 and b"levels" in lib.nerf_last_error()
+    assert lib.nerf_depth_normalize(None, 0, None, None, 0, None) == 0            # empty: no-op
+    assert lib.nerf_depth_normalize(None, 5, None, None, 0, None) == 1
 
 
 def host_pack(state):
