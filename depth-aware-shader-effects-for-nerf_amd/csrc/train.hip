@@ -522,6 +522,214 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   }
 }
 
+// The weight-gradient kernel of the split MLP arithmetic ("bf16x6", nerf_arith F16X3): the same
+// partial sums as wgrad_lds_kernel, on v_mfma_f32_32x32x16_bf16.  Every operand value is split into
+// three bf16 parts, x = b0 + b1 + b2 + O(2^-27 x) (each part the RNE bf16 of the f32 remainder, the
+// remainders exact), and a k-step accumulates the six products of order >= 2^-16,
+//   b0c2 + b1c1 + b2c0 + b0c1 + b1c0 + b0c0   (small terms first; dropped ones O(2^-24)),
+// so the result has fp32-level error, at 6 x 32 MFMA cycles per 16 samples against 8 x 64 for
+// v_mfma_f32_32x32x2_f32.  bf16 has f32's exponent range: no scaling (gradient rows reach 1e-9).
+// A workgroup computes a (64 WN) x (64 WK) tile of one 2048-sample chunk; 16-sample stages are
+// split by the loader (a thread owns 8 samples of one column: 8 coalesced dword loads, three
+// 16-byte LDS writes) into [part][column][sample] rows of 24 bf16 (48-byte stride: the MFMA
+// operand reads, 16 bytes per lane from 16 consecutive rows, are bank-conflict free), double
+// buffered with the next stage's loads in flight during the MFMAs.  The bias column sums the
+// loader's f32 values.  Workgroups sharing a chunk are launched 8 apart (same XCD).
+constexpr int kBfStage = 16;   // samples per stage = one MFMA k-step
+constexpr int kBfRow = 24;     // bf16 per LDS row (16 samples + pad)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int WN, int WK>
+__global__ void __launch_bounds__(256, WN == 4 ? 1 : 2)   // 256 x 64 tiles: 94 KB of LDS, one block per CU
+wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
+                int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
+  static_assert(WN * WK == 4, "four waves");
+  constexpr int BN = 64 * WN, BK = 64 * WK;
+  constexpr int SA = 2 * BN / 256 > 0 ? 2 * BN / 256 : 1;    // loader slots per thread (column, octet)
+  constexpr int SX = 2 * BK / 256 > 0 ? 2 * BK / 256 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BN][kBfRow];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BK][kBfRow];
+  __shared__ float bsum[2][BN];
+  const int b = blockIdx.x;
+  const int grp = b / (8 * tiles), rem = b % (8 * tiles);
+  const int chunk = grp * 8 + (rem & 7);
+  const int tile = rem >> 3;
+  if (chunk >= chunks) return;                     // uniform over the block, before any barrier
+  const int n0 = (tile / ntk) * BN, k0 = (tile % ntk) * BK;
+  const bool do_bias = (tile % ntk) == 0;
+  const int64_t m0 = (int64_t)chunk * kWChunk;
+  const int64_t m1 = m0 + kWChunk < M ? m0 + kWChunk : M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wn = w % WN, wk = w / WN;
+  float ra[SA][8], rx[SX][8];
+  float bacc[SA];
+#pragma unroll
+  for (int q = 0; q < SA; ++q) bacc[q] = 0.0f;
+  // Operands through buffer loads (an out-of-range offset reads 0, so no branches in the loader).
+  // a: one resource per stage, based at the stage's first row, sized to the chunk's remaining rows;
+  // a slot's sample j sits at byte aoff + j*lda4 (past the resource for samples >= m1), and a
+  // column >= N gets an offset >= 2^31 (> any resource size: host-checked lda < 2^18).
+  // x: based at the chunk's first x row; sample m reads row xrow(m) - xrow(m0) = (r0 + rel) / xd
+  // (rel = m - m0, r0 = m0 % xd; xd = 1 per sample, N per ray, "infinite" for one broadcast row),
+  // stepped over a slot's 8 samples by a carry instead of a division.
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  constexpr uint32_t kOut = 0x80000000u;
+  uint32_t aoff[SA], xcol[SX];
+#pragma unroll
+  for (int q = 0; q < SA; ++q) {
+    const int slot = tid + 256 * q, col = slot % BN, oct = slot / BN;
+    aoff[q] = (slot < 2 * BN && n0 + col < N) ? (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)(n0 + col) : kOut;
+  }
+#pragma unroll
+  for (int q = 0; q < SX; ++q) {
+    const int slot = tid + 256 * q, col = slot % BK;
+    xcol[q] = (slot < 2 * BK && k0 + col < K) ? 4u * (uint32_t)(k0 + col) : kOut;
+  }
+  const uint32_t xd = x_div == 0 ? 0xFFFFFFFFu : (uint32_t)x_div;
+  const int64_t xr0 = x_div == 0 ? 0 : m0 / x_div;
+  const uint32_t r0 = x_div == 0 ? 0u : (uint32_t)(m0 - xr0 * x_div);
+  const uint32_t xrows = x_div == 0 ? 1u : (uint32_t)((m1 - 1) / x_div - xr0 + 1);
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + xr0 * ldx), (short)0, (int)(xrows * ldx4), 0x00020000);
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  auto load = [&](int stage) __attribute__((always_inline)) {
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage);
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+#pragma unroll
+    for (int q = 0; q < SA; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        ra[q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)(aoff[q] + j * lda4), 0, 0));
+#pragma unroll
+    for (int q = 0; q < SX; ++q) {
+      const int slot = tid + 256 * q, oct = slot / BK;
+      const uint32_t rel = rel0 + 8u * (uint32_t)oct;
+      uint32_t row = (r0 + rel) / xd, r = (r0 + rel) - row * xd;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = rel + j < mrel_end && xcol[q] != kOut;
+        const uint32_t off = ok ? row * ldx4 + xcol[q] : kOut;
+        rx[q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)off, 0, 0));
+        if (++r == xd) {
+          r = 0;
+          ++row;
+        }
+      }
+    }
+  };
+  auto split_store = [&](float (&v)[8], __bf16 (*dst)[kBfRow], int col, int oct, int plane_stride) {
+    bf16x8 p0, p1, p2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 h0 = (__bf16)v[j];
+      const float r1 = v[j] - (float)h0;
+      const __bf16 h1 = (__bf16)r1;
+      const float r2 = r1 - (float)h1;
+      p0[j] = h0;
+      p1[j] = h1;
+      p2[j] = (__bf16)r2;
+    }
+    *reinterpret_cast<bf16x8*>(&dst[col][8 * oct]) = p0;
+    *reinterpret_cast<bf16x8*>(&dst[col + plane_stride][8 * oct]) = p1;
+    *reinterpret_cast<bf16x8*>(&dst[col + 2 * plane_stride][8 * oct]) = p2;
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < SA; ++q) {
+      const int slot = tid + 256 * q, col = slot % BN, oct = slot / BN;
+      if (slot < 2 * BN) {
+        if (do_bias) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[q] += ra[q][j];
+        }
+        split_store(ra[q], &As[buf][0][0], col, oct, BN);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < SX; ++q) {
+      const int slot = tid + 256 * q, col = slot % BK, oct = slot / BK;
+      if (slot < 2 * BK) split_store(rx[q], &Xs[buf][0][0], col, oct, BK);
+    }
+  };
+  const bool n_act0 = n0 + 64 * wn < N, n_act1 = n0 + 64 * wn + 32 < N;
+  const bool k_act0 = k0 + 64 * wk < K, k_act1 = k0 + 64 * wk + 32 < K;
+  f32x16 acc[2][2] = {{f32x16{}, f32x16{}}, {f32x16{}, f32x16{}}};
+  const int nstages = (int)((m1 - m0 + kBfStage - 1) / kBfStage);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int h = lane >> 5, c = lane & 31;
+  for (int st = 0; st < nstages; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nstages) load(st + 1);
+    if (n_act0 && k_act0) {
+      bf16x8 fa[2][3], fx[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          fa[i][p] = *reinterpret_cast<const bf16x8*>(&As[buf][p][64 * wn + 32 * i + c][8 * h]);
+          fx[i][p] = *reinterpret_cast<const bf16x8*>(&Xs[buf][p][64 * wk + 32 * i + c][8 * h]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if ((i == 1 && !n_act1) || (j == 1 && !k_act1)) continue;
+          f32x16 t = acc[i][j];
+          t = mfma_bf16(fa[i][0], fx[j][2], t);
+          t = mfma_bf16(fa[i][1], fx[j][1], t);
+          t = mfma_bf16(fa[i][2], fx[j][0], t);
+          t = mfma_bf16(fa[i][0], fx[j][1], t);
+          t = mfma_bf16(fa[i][1], fx[j][0], t);
+          acc[i][j] = mfma_bf16(fa[i][0], fx[j][0], t);
+        }
+    }
+    if (st + 1 < nstages) store(buf ^ 1);
+    __syncthreads();
+  }
+  const int KP = K + 1;
+  float* out = partial + (size_t)chunk * wgrad_stride(N, K);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = k0 + 64 * wk + 32 * j + c;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int nn = n0 + 64 * wn + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        if (nn < N && kk < K) out[(size_t)nn * KP + kk] = acc[i][j][g];
+      }
+    }
+  if (do_bias) {
+    // every staged a value passed through store() exactly once (the prologue stores stage 0)
+#pragma unroll
+    for (int q = 0; q < SA; ++q) {
+      const int slot = tid + 256 * q, col = slot % BN, oct = slot / BN;
+      if (slot < 2 * BN) bsum[oct][col] = bacc[q];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < N) out[(size_t)(n0 + tid) * KP + K] = bsum[0][tid] + bsum[1][tid];
+  }
+}
+
+template <int WN, int WK>
+static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
+                           int64_t M, int chunks, float* ws, hipStream_t s) {
+  const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
+  const int tiles = ntn * ntk;
+  const int blocks = ((chunks + 7) / 8) * 8 * tiles;
+  hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div,
+                     M, ntk, tiles, chunks, ws);
+  return check_launch("wgrad_bf_kernel");
+}
+
 // out_w[n][k] (ld K) and out_b[n] (nullable) = (accumulate ? out : 0) + sum over chunks, in chunk
 // order.  A workgroup owns 64 float4 columns of the partial layout; its 4 waves each sum a
 // quarter of the chunks (fixed order), then the quarters are added in order: deterministic.
@@ -586,7 +794,11 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   const int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
   int rc;
-  if (aligned && K >= 1 && K <= 64 && N > 64)
+  // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
+  if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
+    if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+    else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+  } else if (aligned && K >= 1 && K <= 64 && N > 64)
     rc = launch_wgrad_lds<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
   else if (aligned && K >= 1)
     rc = launch_wgrad_lds<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
