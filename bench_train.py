@@ -17,9 +17,9 @@ roofline: per-sample algorithmic FLOP of the three MFMA kernels (forward 1,048,8
 gradients 983,040; weight gradients 1,066,752 including bias columns — DESIGN.md §Training)
 over their event-timed durations.  The forward runs on the MLP arithmetic selected by --arith
 (f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
-157.3).  The data gradients run on fp32 MFMA (peak 157.3 TFLOP/s); the weight gradients run on
-bf16x6 MFMA under f16x3 (six bf16 products per fp32 product: 2516.8/6 = 419.5 TFLOP/s) and on
-fp32 MFMA under f32.
+157.3).  Under f16x3 the data gradients run on split-f16 MFMA too (838.9) and the weight
+gradients on bf16x6 MFMA (six bf16 products per fp32 product: 2516.8/6 = 419.5 TFLOP/s); under
+f32 both run on fp32 MFMA (157.3).
 cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on a 1024-ray
 batch on this host's cores.
 """
@@ -154,7 +154,7 @@ def main():
         kern = {"mlp_forward_train": (FLOP_FWD, kt["mlp_forward_ms"]), "mlp_backward": (FLOP_DGRAD, kt["mlp_backward_ms"]),
                 "wgrad": (FLOP_WGRAD, kt["param_grads_ms"])}
         peaks = {"mlp_forward_train": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
-                 "mlp_backward": MFMA_F32_PEAK_TFLOPS,
+                 "mlp_backward": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
                  "wgrad": MFMA_F32_PEAK_TFLOPS * (16 / 6 if args.arith == "f16x3" else 1)}
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]

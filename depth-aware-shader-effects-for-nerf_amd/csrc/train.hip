@@ -13,6 +13,7 @@
 //                               batch, chunked over samples with a deterministic reduction
 //   app_grad_kernel             per-ray appearance-embedding gradient
 //   adam_kernel                 torch.optim.Adam's update, element for element
+#include <cstring>
 #include <utility>
 
 #include "common.h"
@@ -145,7 +146,18 @@ int launch_composite_backward(const float* rgb, const float* sigma, const float*
 // in registers, exactly like the forward.
 NERF_HD constexpr int tmat_ksteps(int mt) { return mt == 7 ? kDirHidden / 2 : kActSteps; }
 NERF_HD constexpr size_t tmat_offset(int mt) { return (size_t)mt * 8 * kActSteps * 64; }
-constexpr size_t kPackedTFloats = tmat_offset(7) + (size_t)8 * (kDirHidden / 2) * 64;   // 491520
+constexpr size_t kPackedT32Floats = tmat_offset(7) + (size_t)8 * (kDirHidden / 2) * 64;   // 491520
+// Split-f16 part (mlp_backward16_kernel), after the f32 part: W^T s_w of the same 8 matrices as f16
+// hi/lo A fragments of v_mfma_f32_32x32x16_f16.  Matrix mt holds 2 tile groups x KS16 k-steps x
+// 4 tiles x {hi, lo} pieces, each 64 lanes x 8 halves (4 words); the kernel streams them in that
+// order.  Lane l of the piece for (tile tt, k-step ks) holds W^T[32 tt + (l & 31)][n_j], the
+// k index n_j = 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 (l >> 5) + (j & 3) being the
+// accumulator order in which the previous backward layer leaves its outputs (act_feature).
+// s_w = 2^(14 - e) with max |W| < 2^e per matrix (layout.h s16_exponent), and its inverse, follow.
+NERF_HD constexpr int t16_ksteps(int mt) { return mt == 7 ? kDirHidden / 16 : kHidden / 16; }
+NERF_HD constexpr size_t t16_offset(int mt) { return kPackedT32Floats + (size_t)mt * 2 * 16 * 8 * 256; }
+constexpr size_t kOffT16Consts = t16_offset(7) + (size_t)2 * 8 * 8 * 256;   // s_w[8], 1/s_w[8]
+constexpr size_t kPackedTFloats = kOffT16Consts + 16;                         // 983056
 
 NERF_HD inline float packT_value(const float* const* P, size_t e) {
   int mt = (int)(e / (8 * kActSteps * 64));
@@ -164,25 +176,105 @@ NERF_HD inline float packT_value(const float* const* P, size_t e) {
   return P[2 * layer][(size_t)o * K + i];
 }
 
+// W^T[i][o] of matrix mt (forward input neuron i, output neuron o)
+NERF_HD inline float tmat_weight(const float* const* P, int mt, int i, int o) {
+  if (mt == 7) return P[P_DIR_W][(size_t)o * (kHidden + kDirEnc) + i];
+  const int layer = mt + 1;
+  const int K = layer == kSkipLayer ? kHidden + kPosEnc : kHidden;
+  return P[2 * layer][(size_t)o * K + i];
+}
+
+// max |W^T| of matrix mt over rows i (one thread per row)
+NERF_HD inline float tmat_row_max(const float* const* P, int mt, int i) {
+  const int outs = mt == 7 ? kDirHidden : kHidden;
+  float m = 0.0f;
+  for (int o = 0; o < outs; ++o) m = fmaxf(m, fabsf(tmat_weight(P, mt, i, o)));
+  return m;
+}
+
+NERF_HD inline void store_t16_consts(float* consts, int mt, float mx) {
+  const int e = s16_exponent(mx);
+  consts[mt] = ldexpf(1.0f, 14 - e);
+  consts[8 + mt] = ldexpf(1.0f, e - 14);
+}
+
+// word w (two halves) of the split-f16 part, w relative to t16_offset(0)
+NERF_HD inline uint32_t packT16_word(const float* const* P, const float* consts, size_t w) {
+  int mt = (int)(w / (2 * 16 * 8 * 256));
+  if (mt > 7) mt = 7;
+  const size_t rel = w - (t16_offset(mt) - kPackedT32Floats);
+  const int KS = t16_ksteps(mt);
+  const int jj = (int)(rel & 3), lane = (int)((rel >> 2) & 63);
+  const size_t piece = rel >> 8;
+  const int part = (int)(piece & 1), i = (int)((piece >> 1) & 3);
+  const int step = (int)(piece >> 3), g = step / KS, ks = step % KS;
+  const int row = 32 * (4 * g + i) + (lane & 31);
+  uint32_t word = 0;
+  for (int k = 0; k < 2; ++k) {
+    const int j = 2 * jj + k;
+    const int o = 32 * (ks >> 1) + 16 * (ks & 1) + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+    const float v = tmat_weight(P, mt, row, o) * consts[mt];
+    const _Float16 hi = (_Float16)v;
+    const _Float16 out = part == 0 ? hi : (_Float16)(v - (float)hi);
+    uint16_t bits;
+    memcpy(&bits, &out, 2);
+    word |= (uint32_t)bits << (16 * k);
+  }
+  return word;
+}
+
 struct ParamPtrsT { const float* p[P_COUNT]; };
 
 __global__ void __launch_bounds__(256) packT_kernel(ParamPtrsT P, float* __restrict__ packed) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < kPackedTFloats) packed[e] = packT_value(P.p, e);
+  if (e < kPackedT32Floats) packed[e] = packT_value(P.p, e);
+}
+
+// one block per matrix: s_w and 1/s_w
+__global__ void __launch_bounds__(256) scaleT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
+  __shared__ float red[256];
+  red[threadIdx.x] = tmat_row_max(P.p, blockIdx.x, threadIdx.x);
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) store_t16_consts(packed + kOffT16Consts, blockIdx.x, red[0]);
+}
+
+__global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
+  const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < kOffT16Consts - kPackedT32Floats)
+    reinterpret_cast<uint32_t*>(packed)[kPackedT32Floats + w] = packT16_word(P.p, packed + kOffT16Consts, w);
 }
 
 int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
   ParamPtrsT P;
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
-  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedTFloats + 255) / 256)), dim3(256), 0, s, P, packedT);
-  return check_launch("packT_kernel");
+  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256)), dim3(256), 0, s, P, packedT);
+  if (int rc = check_launch("packT_kernel")) return rc;
+  hipLaunchKernelGGL(scaleT16_kernel, dim3(8), dim3(256), 0, s, P, packedT);
+  if (int rc = check_launch("scaleT16_kernel")) return rc;
+  const size_t words = kOffT16Consts - kPackedT32Floats;
+  hipLaunchKernelGGL(packT16_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, packedT);
+  return check_launch("packT16_kernel");
 }
 
 void packT_host(const float* const* params, float* packedT) {
-  for (size_t e = 0; e < kPackedTFloats; ++e) packedT[e] = packT_value(params, e);
+  for (size_t e = 0; e < kPackedT32Floats; ++e) packedT[e] = packT_value(params, e);
+  float* consts = packedT + kOffT16Consts;
+  for (int mt = 0; mt < 8; ++mt) {
+    float mx = 0.0f;
+    for (int i = 0; i < kHidden; ++i) mx = fmaxf(mx, tmat_row_max(params, mt, i));
+    store_t16_consts(consts, mt, mx);
+  }
+  uint32_t* words = reinterpret_cast<uint32_t*>(packedT);
+  for (size_t w = 0; w < kOffT16Consts - kPackedT32Floats; ++w)
+    words[kPackedT32Floats + w] = packT16_word(params, consts, w);
 }
 
 // ------------------------------------------------------------------------------ MLP backward
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x16 mfma32t(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -235,11 +327,31 @@ __device__ __forceinline__ void dgrad(const float* __restrict__ wmat, const f32x
   });
 }
 
+// A wave's 32 gradient rows as a buffer resource sized to the rows that exist, so the stores of
+// tail lanes fall outside it and are dropped: no branches around stores, which would otherwise
+// split the loads and stores of the ReLU backward into one memory round trip per 16 bytes.
+struct GradRows {
+  __amdgpu_buffer_rsrc_t res;
+  uint32_t loff;   // this lane's byte offset: row (lane & 31), lane half h
+};
+
+__device__ __forceinline__ GradRows grad_rows(float* grad, int64_t s0, int64_t M, int lane) {
+  const int64_t rows = M - s0 < 32 ? M - s0 : 32;
+  GradRows g;
+  g.res = __builtin_amdgcn_make_buffer_rsrc(grad + s0 * kGradRow, (short)0, (int)(rows * kGradRow * 4), 0x00020000);
+  g.loff = (uint32_t)(lane & 31) * (kGradRow * 4) + 16u * (uint32_t)(lane >> 5);
+  return g;
+}
+
+// 16 bytes at float offset off (+ 4 h) of this lane's gradient row
+__device__ __forceinline__ void grad_store4(const GradRows& g, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), g.res, (int)g.loff, 4 * off, 0);
+}
+
 // d pre-activation = d activation * [activation > 0] (ReLU backward; the saved activation is
 // ReLU(pre), positive exactly where pre is), in place, and stored to the gradient row.
 __device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, const float* __restrict__ srow,
-                                                int save_off, float* __restrict__ grow, int grad_off, int h,
-                                                bool valid) {
+                                                int save_off, const GradRows& gr, int grad_off, int h) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     if (t >= ntiles) break;
@@ -253,7 +365,7 @@ __device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, cons
         x[t][4 * q + e] = d;
         v[e] = d;
       }
-      if (valid) *reinterpret_cast<f32x4*>(grow + grad_off + t * 32 + 8 * q + 4 * h) = v;
+      grad_store4(gr, grad_off + t * 32 + 8 * q, v);
     }
   }
 }
@@ -264,13 +376,14 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
                     const float* __restrict__ dsigma, const float* __restrict__ drgb, int64_t M,
                     float* __restrict__ grad) {
   const int lane = threadIdx.x & 63;
-  const int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
+  const int64_t s0 = ((int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 32;   // wave-uniform
   if (s0 >= M) return;
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const bool valid = s0 + (lane & 31) < M;
   const float* srow = save + s * kSaveRow;
   float* grow = grad + s * kGradRow;
+  const GradRows gr = grad_rows(grad, s0, M, lane);
 
   // rgb head: rgb = sigmoid(v) -> dv = drgb * rgb (1 - rgb) (models.py:159-160)
   float dv[3];
@@ -301,10 +414,10 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
         A[t][4 * q + e] = d;
         v[e] = d;
       }
-      if (valid) *reinterpret_cast<f32x4*>(grow + kGradHd + t * 32 + 8 * q + 4 * h) = v;
+      grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
     }
   // hd = ReLU(dir pre) + appearance: d dir_pre = d hd * [r_dir > 0]
-  relu_back_store(A, 4, srow, kSaveRDir, grow, kGradDir, h, valid);
+  relu_back_store(A, 4, srow, kSaveRDir, gr, kGradDir, h);
   // d h7 = W_dh^T d dir_pre + w_sigma * d v_s
   dgrad<kDirHidden / 2>(packedT + tmat_offset(7), A, B, lane);
   const float* wsg = packed + kOffSigmaW;
@@ -320,20 +433,179 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
 #pragma unroll 1
   for (int p = 0; p < 3; ++p) {
     const int l1 = 7 - 2 * p, l2 = 6 - 2 * p;
-    relu_back_store(B, 8, srow, save_h(l1), grow, l1 * kHidden, h, valid);
+    relu_back_store(B, 8, srow, save_h(l1), gr, l1 * kHidden, h);
     dgrad<kActSteps>(packedT + tmat_offset(l1 - 1), B, A, lane);
-    relu_back_store(A, 8, srow, save_h(l2), grow, l2 * kHidden, h, valid);
+    relu_back_store(A, 8, srow, save_h(l2), gr, l2 * kHidden, h);
     dgrad<kActSteps>(packedT + tmat_offset(l2 - 1), A, B, lane);
   }
-  relu_back_store(B, 8, srow, save_h(1), grow, 1 * kHidden, h, valid);
+  relu_back_store(B, 8, srow, save_h(1), gr, 1 * kHidden, h);
   dgrad<kActSteps>(packedT + tmat_offset(0), B, A, lane);
-  relu_back_store(A, 8, srow, save_h(0), grow, 0, h, valid);
+  relu_back_store(A, 8, srow, save_h(0), gr, 0, h);
+}
+
+// ---------------------------------------------------------------- MLP backward, split f16
+// The same chain on v_mfma_f32_32x32x16_f16 (nerf_arith F16X3), the arithmetic of mlp16_kernel:
+// out = W^T g as hi(W s_w) hi(g s_g) + hi(W s_w) lo(g s_g) + lo(W s_w) hi(g s_g) with f32
+// accumulation, unscaled by the exact inverses.  x s = hi + lo + O(2^-24 |x s|) for both operands
+// and the dropped lo lo term is O(2^-22) of the products, so the result has fp32-level error.
+// s_w is per matrix (pack time, packedT's split part); s_g is per sample, from the exact max |g|
+// over the sample's gradient row (both lane halves): the whole row exists before the layer starts,
+// so no bound is needed.  s_g = 2^(140 - E), E the biased exponent of the max (>= 14, so s_g stays
+// a normal float): |g s_g| < 2^14.  Each 16-deep k-step is 3 x 32 MFMA cycles against 8 x 64 for
+// v_mfma_f32_32x32x2_f32.  Weights stream per wave from L2 through a 3-step register ring (one
+// step = 4 tiles x {hi, lo} = 8 KiB for 12 MFMAs).
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma16t(u32x4 a, h16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h16x8, a), b, c, 0, 0, 0);
+}
+
+// Split tiles 0..NT-1 of X (k-steps 2t + s: accumulator elements 8s..8s+7) at the sample's scale;
+// returns 1 / s_g.
+template <int NT>
+__device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16], h16x8 (&bl)[16]) {
+  float m = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) m = fmaxf(m, fabsf(X[t][g]));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  int E = (int)((__float_as_uint(m) >> 23) & 0xffu);
+  E = E < 14 ? 14 : E;
+  const float sc = __uint_as_float((uint32_t)(267 - E) << 23);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = X[t][8 * q + j] * sc;
+        const _Float16 hi = (_Float16)v;
+        bh[2 * t + q][j] = hi;
+        bl[2 * t + q][j] = (_Float16)(v - (float)hi);
+      }
+  return __uint_as_float((uint32_t)(E - 13) << 23);
+}
+
+// out (8 tiles) = (W^T g) from the split operands of KS k-steps; inv_w = 1/s_w, inv_g = 1/s_g.
+template <int KS>
+__device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const h16x8 (&bh)[16],
+                                        const h16x8 (&bl)[16], f32x16 (&out)[8], float inv_w, float inv_g,
+                                        int lane) {
+  constexpr int STEPS = 2 * KS, PIECES = 8 * STEPS, DEPTH = 24;
+  const u32x4* __restrict__ wf = reinterpret_cast<const u32x4*>(wmat) + lane;
+  u32x4 ring[DEPTH];
+#pragma unroll
+  for (int p = 0; p < DEPTH; ++p) ring[p] = wf[p * 64];
+  sfor<STEPS>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int st = decltype(sc)::value;
+    constexpr int g = st / KS, ks = st % KS;
+    if constexpr (ks == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[4 * g + i] = f32x16{};
+    }
+    // small products first: lo(W) hi(g), hi(W) lo(g), then hi(W) hi(g); tiles interleaved
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * g + i] = mfma16t(ring[(8 * st + 2 * i + 1) % DEPTH], bh[ks], out[4 * g + i]);
+    });
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * g + i] = mfma16t(ring[(8 * st + 2 * i) % DEPTH], bl[ks], out[4 * g + i]);
+    });
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * g + i] = mfma16t(ring[(8 * st + 2 * i) % DEPTH], bh[ks], out[4 * g + i]);
+    });
+    sfor<8>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int p = 8 * st + decltype(qc)::value;
+      if constexpr (p + DEPTH < PIECES) ring[p % DEPTH] = wf[(p + DEPTH) * 64];
+    });
+    if constexpr (ks == KS - 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[4 * g + i] = (out[4 * g + i] * inv_w) * inv_g;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+__global__ void __launch_bounds__(256, 1)
+mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
+                      const float* __restrict__ save, const float* __restrict__ sigma, const float* __restrict__ rgb,
+                      const float* __restrict__ dsigma, const float* __restrict__ drgb, int64_t M,
+                      float* __restrict__ grad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s0 = ((int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 32;   // wave-uniform
+  if (s0 >= M) return;
+  const int h = lane >> 5;
+  const int64_t s = imin64(s0 + (lane & 31), M - 1);
+  const bool valid = s0 + (lane & 31) < M;
+  const float* srow = save + s * kSaveRow;
+  float* grow = grad + s * kGradRow;
+  const GradRows gr = grad_rows(grad, s0, M, lane);
+  const uint32_t* t16 = reinterpret_cast<const uint32_t*>(packedT);
+  const float* invw = packedT + kOffT16Consts + 8;
+
+  // heads, as mlp_backward_kernel
+  float dv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float y = rgb[3 * s + c];
+    dv[c] = drgb[3 * s + c] * (y * (1.0f - y));
+  }
+  const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
+  if (valid && h == 0) {
+    grow[kGradSigma] = dsp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+  }
+  f32x16 X[8];
+  h16x8 bh[16], bl[16];
+  const float* wr = packed + kOffRgbW;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = t * 32 + 8 * q + 4 * h + e;
+        const float d = fmaf(dv[2], wr[2 * kDirHidden + n], fmaf(dv[1], wr[kDirHidden + n], dv[0] * wr[n]));
+        X[t][4 * q + e] = d;
+        v[e] = d;
+      }
+      grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
+    }
+  relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
+  float inv_g = split_rows<4>(X, bh, bl);
+  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, lane);
+  const float* wsg = packed + kOffSigmaW;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wsg + t * 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) X[t][4 * q + e] = fmaf(dsp, w[e], X[t][4 * q + e]);
+    }
+#pragma unroll 1
+  for (int l = 7; l >= 1; --l) {
+    relu_back_store(X, 8, srow, save_h(l), gr, l * kHidden, h);
+    inv_g = split_rows<8>(X, bh, bl);
+    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, lane);
+  }
+  relu_back_store(X, 8, srow, save_h(0), gr, 0, h);
 }
 
 int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
                         const float* rgb, const float* dsigma, const float* drgb, int64_t M, float* grad,
                         hipStream_t s) {
   if (M == 0) return NERF_OK;
+  if (g_mlp_arith == NERF_ARITH_F16X3) {
+    hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT,
+                       save, sigma, rgb, dsigma, drgb, M, grad);
+    return check_launch("mlp_backward16_kernel");
+  }
   hipLaunchKernelGGL(mlp_backward_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT, save,
                      sigma, rgb, dsigma, drgb, M, grad);
   return check_launch("mlp_backward_kernel");

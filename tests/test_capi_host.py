@@ -361,7 +361,7 @@ def tfrag_matrix(packedT, mt):
 
 def test_transposed_fragments_are_permuted_weight_transposes(ref_state):
     packedT = host_pack_transposed(ref_state)
-    assert packedT.size == 7 * 256 * 256 + 256 * 128
+    assert packedT.size == 2 * (7 * 256 * 256 + 256 * 128) + 16
     for layer in range(1, 8):
         W = ref_state[f"pts_linears.{layer}.weight"].numpy()[:, :256]        # [out][in]
         cols = [act_feature(s // 2, s % 2) for s in range(256)]
@@ -369,6 +369,38 @@ def test_transposed_fragments_are_permuted_weight_transposes(ref_state):
     Wd = ref_state["dir_linear.weight"].numpy()[:, :256]                     # (128, 256)
     cols = [act_feature(s // 2, s % 2) for s in range(128)]
     assert np.array_equal(tfrag_matrix(packedT, 7), Wd.T[:, cols])
+
+
+def test_transposed_split_f16_fragments(ref_state):
+    """The split-f16 part of packedT (mlp_backward16_kernel): per matrix a power-of-two s_w with
+    max |W s_w| < 2^14, hi = f16(W s_w) and lo = f16(W s_w - hi) in fragment order
+    [group][k-step][tile][hi, lo][lane][8 halves], k index 32 (ks>>1) + 16 (ks&1) + 8 (j>>2) + 4 h + (j&3)."""
+    packedT = host_pack_transposed(ref_state)
+    base = 7 * 256 * 256 + 256 * 128
+    consts = packedT[2 * base: 2 * base + 16]
+    words = packedT[base: 2 * base].view(np.float16)
+    off = 0
+    for mt in range(8):
+        if mt < 7:
+            W = ref_state[f"pts_linears.{mt + 1}.weight"].numpy()[:, :256]       # [out][in]
+        else:
+            W = ref_state["dir_linear.weight"].numpy()[:, :256]
+        WT = W.T.astype(np.float64)                                              # [in][out]
+        sw, inv = float(consts[mt]), float(consts[8 + mt])
+        assert sw * inv == 1.0 and np.log2(sw) == int(np.log2(sw))
+        assert np.abs(WT).max() * sw < 2 ** 14 and np.abs(WT).max() * sw >= 2 ** 13
+        KS = 16 if mt < 7 else 8
+        n = 2 * KS * 4 * 2 * 64 * 8
+        blk = words[off: off + n].astype(np.float64).reshape(2, KS, 4, 2, 2, 32, 8)   # g ks i part h c j
+        off += n
+        g, ks, i, h, c, j = np.meshgrid(np.arange(2), np.arange(KS), np.arange(4), np.arange(2), np.arange(32),
+                                        np.arange(8), indexing="ij")
+        row = 32 * (4 * g + i) + c
+        col = 32 * (ks >> 1) + 16 * (ks & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+        exp = WT[row, col] * sw
+        hi, lo = blk[:, :, :, 0], blk[:, :, :, 1]
+        assert np.array_equal(hi, exp.astype(np.float16).astype(np.float64)), mt
+        assert np.abs(hi + lo - exp).max() <= 2.0 ** -10, mt      # |W s_w| < 2^14: split residual < 2^-11
 
 
 def emulate_backward(packed, packedT, x, d, app, g_rgb, g_sigma):
