@@ -357,7 +357,11 @@ __device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, cons
     if (t >= ntiles) break;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+#ifdef NERF_BW16_ABL_SAVE      // timing only: no activation loads
+      const f32x4 a = {x[t][4 * q], x[t][4 * q + 1], x[t][4 * q + 2], x[t][4 * q + 3]};
+#else
       const f32x4 a = *reinterpret_cast<const f32x4*>(srow + save_off + t * 32 + 8 * q + 4 * h);
+#endif
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -488,18 +492,39 @@ __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16
 }
 
 // out (8 tiles) = (W^T g) from the split operands of KS k-steps; inv_w = 1/s_w, inv_g = 1/s_g.
+// Meanwhile the output's ReLU mask is fetched: the 128 saved activations this lane needs next
+// (act, 32 chunks of 4 at act + 32 t + 8 q) are loaded a few per step and folded into 128 bits
+// (chunk c = 4 t + q, element e -> bit 4 c + e), so the ReLU backward waits for no load.
+__device__ __forceinline__ void fold_mask(uint32_t (&mask)[4], int c, f32x4 a) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) mask[c / 8] |= (a[e] > 0.0f ? 1u : 0u) << (4 * (c % 8) + e);
+}
+
 template <int KS>
 __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const h16x8 (&bh)[16],
                                         const h16x8 (&bl)[16], f32x16 (&out)[8], float inv_w, float inv_g,
-                                        int lane) {
+                                        const float* __restrict__ act, uint32_t (&mask)[4], int lane) {
   constexpr int STEPS = 2 * KS, PIECES = 8 * STEPS, DEPTH = 24;
+  constexpr int CPS = 32 / STEPS, LAG = 3, RS = (LAG + 1) * CPS;   // mask chunks per step, load->fold lag
   const u32x4* __restrict__ wf = reinterpret_cast<const u32x4*>(wmat) + lane;
   u32x4 ring[DEPTH];
+  f32x4 pf[RS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mask[i] = 0u;
 #pragma unroll
   for (int p = 0; p < DEPTH; ++p) ring[p] = wf[p * 64];
   sfor<STEPS>([&](auto sc) __attribute__((always_inline)) {
     constexpr int st = decltype(sc)::value;
     constexpr int g = st / KS, ks = st % KS;
+    if constexpr (st >= LAG) {
+#pragma unroll
+      for (int u = 0; u < CPS; ++u) fold_mask(mask, (st - LAG) * CPS + u, pf[((st - LAG) * CPS + u) % RS]);
+    }
+#pragma unroll
+    for (int u = 0; u < CPS; ++u) {
+      const int c = st * CPS + u;
+      pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
+    }
     if constexpr (ks == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[4 * g + i] = f32x16{};
@@ -519,7 +544,11 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
     });
     sfor<8>([&](auto qc) __attribute__((always_inline)) {
       constexpr int p = 8 * st + decltype(qc)::value;
+#ifdef NERF_BW16_ABL_WEIGHTS   // timing only: every step re-reads the first 24 pieces (L1-resident)
+      if constexpr (p + DEPTH < PIECES) ring[p % DEPTH] = wf[((p + DEPTH) % DEPTH) * 64];
+#else
       if constexpr (p + DEPTH < PIECES) ring[p % DEPTH] = wf[(p + DEPTH) * 64];
+#endif
     });
     if constexpr (ks == KS - 1) {
 #pragma unroll
@@ -527,6 +556,27 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
     }
     __builtin_amdgcn_sched_barrier(0);
   });
+#pragma unroll
+  for (int c = (STEPS - LAG) * CPS; c < 32; ++c) fold_mask(mask, c, pf[c % RS]);
+}
+
+// relu_back_store with the mask from dgrad16
+__device__ __forceinline__ void relu_mask_store(f32x16 (&x)[8], const uint32_t (&mask)[4], const GradRows& gr,
+                                                int grad_off) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * t + q;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = (mask[c / 8] >> (4 * (c % 8) + e)) & 1u ? x[t][4 * q + e] : 0.0f;
+        x[t][4 * q + e] = d;
+        v[e] = d;
+      }
+      grad_store4(gr, grad_off + t * 32 + 8 * q, v);
+    }
 }
 
 __global__ void __launch_bounds__(256, 1)
@@ -577,8 +627,9 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
       grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
     }
   relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
+  uint32_t mask[4];
   float inv_g = split_rows<4>(X, bh, bl);
-  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, lane);
+  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h, mask, lane);
   const float* wsg = packed + kOffSigmaW;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
@@ -590,11 +641,12 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
     }
 #pragma unroll 1
   for (int l = 7; l >= 1; --l) {
-    relu_back_store(X, 8, srow, save_h(l), gr, l * kHidden, h);
+    relu_mask_store(X, mask, gr, l * kHidden);
     inv_g = split_rows<8>(X, bh, bl);
-    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, lane);
+    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h,
+                          mask, lane);
   }
-  relu_back_store(X, 8, srow, save_h(0), gr, 0, h);
+  relu_mask_store(X, mask, gr, 0);
 }
 
 int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
