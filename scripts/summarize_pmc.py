@@ -22,6 +22,9 @@ for k, cs in per.items():
     if not k.startswith("nerf::"):
         continue
     res["kernels"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
+    kk = res["kernels"][k]
+    if "FETCH_SIZE" in kk and "WRITE_SIZE" in kk:   # same gfx950 correction as the MLP figure below
+        kk["hbm_bytes_per_dispatch"] = (2 * kk["FETCH_SIZE"] + kk["WRITE_SIZE"]) * 1024
 mlp = "nerf::mlp16_kernel" if "nerf::mlp16_kernel" in res["kernels"] else "nerf::mlp_kernel"
 res["mlp_kernel"] = mlp
 m = res["kernels"].get(mlp, {})
