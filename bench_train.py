@@ -79,6 +79,22 @@ def cpu_baseline(target_s):
                       f"train_step on PyTorch-CPU fp32, {t:.1f} s"}
 
 
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary_train.json")
+WGRAD_LAUNCHES = 12   # train.hip param_grads: 11 layer jobs + the appearance projection, each GEMM + reduction
+
+
+def pmc_traffic():
+    """HBM bytes per step of the weight-gradient phase and per data-gradient launch, from the
+    committed PMC passes of `scripts/profile_pmc.sh <dir> train` (2 x FETCH_SIZE + WRITE_SIZE)."""
+    try:
+        k = json.load(open(PMC_SUMMARY))["kernels"]
+        wgrad = WGRAD_LAUNCHES * (k["nerf::wgrad_bf_kernel"]["hbm_bytes_per_dispatch"]
+                                  + k["nerf::wgrad_reduce_kernel"]["hbm_bytes_per_dispatch"])
+        return {"wgrad": wgrad, "mlp_backward": k["nerf::mlp_backward16_kernel"]["hbm_bytes_per_dispatch"]}
+    except (OSError, KeyError, ValueError):
+        return {}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +175,7 @@ def main():
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]
         ach = M * flop / (ms * 1e-3) / 1e12
+        traffic = pmc_traffic() if args.arith == "f16x3" else {}
         out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
                "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -169,7 +186,11 @@ def main():
                           args.batch, "n_samples": cfg.num_samples, "parallelism": f"dp{world} (RCCL all-reduce)"},
                "mlp_arith_forward": args.arith,
                "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": peaks[dominant],
-                            "unit": "TFLOP/s", "frac": ach / peaks[dominant], "traffic": None,
+                            "unit": "TFLOP/s", "frac": ach / peaks[dominant],
+                            "traffic": traffic.get(dominant), "traffic_unit": "bytes/phase (one step)",
+                            "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
+                            if traffic.get(dominant) is not None else None,
+                            "traffic_by_kernel": traffic,
                             "kernels_ms": {k: v[1] for k, v in kern.items()},
                             "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()},
                             "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()}},
