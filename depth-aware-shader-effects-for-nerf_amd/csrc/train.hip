@@ -669,6 +669,16 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
 // (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).  Each chunk's
 // partial occupies wgrad_stride(N, K) floats (N*KP rounded up to 4, for 16-byte reduce loads).
 constexpr int kWChunk = 2048;   // samples per chunk
+// Chunk length of a (N, K) weight gradient on the bf16x6 path: short enough that a 2^18-sample
+// step puts a block in every resident slot.  The 256x64-tile launches (K <= 64, N > 64: layer 0
+// and the appearance projection) hold one block per CU and have one tile: 1024-sample chunks give
+// 256 blocks instead of 128.  The 128x128-tile launches hold two blocks per CU; those with fewer
+// than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
+static inline int wgrad_chunk_len(int N, int K) {
+  if (K <= 64 && N > 64) return kWChunk / 2;
+  const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
+  return tiles == 1 ? kWChunk / 4 : tiles == 2 ? kWChunk / 2 : kWChunk;
+}
 
 NERF_HD inline int64_t wgrad_stride(int N, int K) { return (((int64_t)N * (K + 1)) + 3) & ~(int64_t)3; }
 
@@ -870,7 +880,7 @@ __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
 template <int WN, int WK>
 __global__ void __launch_bounds__(256, WN == 4 ? 1 : 2)   // 256 x 64 tiles: 94 KB of LDS, one block per CU
 wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
-                int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
+                int64_t x_div, int64_t M, int ntk, int tiles, int chunks, int clen, float* __restrict__ partial) {
   static_assert(WN * WK == 4, "four waves");
   constexpr int BN = 64 * WN, BK = 64 * WK;
   constexpr int SA = 2 * BN / 256 > 0 ? 2 * BN / 256 : 1;    // loader slots per thread (column, octet)
@@ -885,8 +895,8 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   if (chunk >= chunks) return;                     // uniform over the block, before any barrier
   const int n0 = (tile / ntk) * BN, k0 = (tile % ntk) * BK;
   const bool do_bias = (tile % ntk) == 0;
-  const int64_t m0 = (int64_t)chunk * kWChunk;
-  const int64_t m1 = m0 + kWChunk < M ? m0 + kWChunk : M;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wn = w % WN, wk = w / WN;
   float ra[SA][8], rx[SX][8];
@@ -1045,12 +1055,12 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
 
 template <int WN, int WK>
 static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
-                           int64_t M, int chunks, float* ws, hipStream_t s) {
+                           int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
   hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div,
-                     M, ntk, tiles, chunks, ws);
+                     M, ntk, tiles, chunks, clen, ws);
   return check_launch("wgrad_bf_kernel");
 }
 
@@ -1096,7 +1106,8 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
 }
 
 size_t wgrad_workspace_floats(int64_t M, int N, int K) {
-  const int64_t chunks = (M + kWChunk - 1) / kWChunk;
+  const int clen = wgrad_chunk_len(N, K);   // >= the chunk count of every path of launch_wgrad
+  const int64_t chunks = (M + clen - 1) / clen;
   return (size_t)chunks * wgrad_stride(N, K);
 }
 
@@ -1115,13 +1126,15 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
                  float* out_w, float* out_b, int accumulate, float* ws, hipStream_t s) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
-  const int chunks = (int)((M + kWChunk - 1) / kWChunk);
+  int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
   int rc;
   // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
-    if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
-    else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+    const int clen = wgrad_chunk_len(N, K);
+    chunks = (int)((M + clen - 1) / clen);
+    if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+    else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
   } else if (aligned && K >= 1 && K <= 64 && N > 64)
     rc = launch_wgrad_lds<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
   else if (aligned && K >= 1)
