@@ -38,6 +38,8 @@ _SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_rng_uniforms": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
     "nerf_packed_weights_floats": (ctypes.c_size_t, []),
     "nerf_set_mlp_arith": (ctypes.c_int, [ctypes.c_int]),
     "nerf_get_mlp_arith": (ctypes.c_int, []),
@@ -88,12 +90,12 @@ _SIGNATURES = {
     "nerf_depth_normalize": (ctypes.c_int, [_V, _I64, _V, _V, ctypes.c_size_t, _V]),
     "nerf_effect_fog": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V, _V,
                                        ctypes.c_size_t, _V]),
-    "nerf_effect_toon": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V,
+    "nerf_effect_toon": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, _V,
                                         _V, ctypes.c_size_t, _V]),
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

@@ -195,7 +195,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 5; }
+int nerf_abi_version(void) { return 6; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -218,6 +218,12 @@ int nerf_positional_encoding(const float* x, int64_t M, int dims, int levels, in
           (long long)M, dims, levels);
   REQUIRE(M == 0 || (x && out), "nerf_positional_encoding: null pointer");
   return launch_pe(x, M, dims, levels, include_input, out, (hipStream_t)stream);
+}
+
+int nerf_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, nerf_stream_t stream) {
+  REQUIRE(first >= 0 && n >= 0, "nerf_rng_uniforms: first=%lld n=%lld", (long long)first, (long long)n);
+  REQUIRE(n == 0 || out, "nerf_rng_uniforms: null pointer");
+  return launch_rng_uniforms(seed, first, n, out, (hipStream_t)stream);
 }
 
 int nerf_sample_stratified(const float* rays_o, const float* rays_d, int64_t B, double near, double far, int N,

@@ -48,6 +48,7 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
 // Kernel launchers (one per translation unit); each returns a nerf_status.
 int launch_get_rays(int H, int W, float focal, const float* c2w, int row0, int nrows,
                     float* o, float* d, hipStream_t s);
+int launch_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, hipStream_t s);
 int launch_pe(const float* x, int64_t M, int dims, int levels, int include_input, float* out, hipStream_t s);
 int launch_normalize(const float* d, int64_t B, float* out, hipStream_t s);
 int launch_stratified(const float* o, const float* d, int64_t B, float near_f, float span_f,

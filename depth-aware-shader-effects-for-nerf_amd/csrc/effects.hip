@@ -56,10 +56,18 @@ __global__ void __launch_bounds__(256) minmax_kernel(const float* __restrict__ x
   }
 }
 
+// Presets mm = {0, ~0} on the stream (a kernel, not a host copy: stream-ordered without a host
+// sync, and capturable into a graph).
+__global__ void minmax_init_kernel(unsigned* __restrict__ mm) {
+  if (threadIdx.x == 0) {
+    mm[0] = 0u;
+    mm[1] = 0xffffffffu;
+  }
+}
+
 static int launch_minmax(const float* x, int64_t n, int64_t stride, unsigned* mm, hipStream_t s) {
-  const unsigned init[2] = {0u, 0xffffffffu};
-  if (hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess)
-    return set_error(NERF_ERR_HIP, "effects: hipMemcpyAsync failed");
+  hipLaunchKernelGGL(minmax_init_kernel, dim3(1), dim3(64), 0, s, mm);
+  if (int rc = check_launch("minmax_init_kernel")) return rc;
   const int64_t blocks = n > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(minmax_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, x, n, stride, mm);
   return check_launch("minmax_kernel");
@@ -76,6 +84,15 @@ __global__ void __launch_bounds__(256) depth_norm_kernel(const float* __restrict
   if (i >= n) return;
   const float mx = ord2f(mm[0]), mn = ord2f(mm[1]);
   out[i] = (d[i] - mn) / ((mx - mn) + 1e-6f);
+}
+
+// a**3.0 rounded once to float: a*a is exact in double (48 significant bits), the second product
+// rounds to double and then to float.  numpy's float32 power is its SIMD pow (SVML on AVX-512
+// hosts, libm elsewhere), within 1 ulp of this and host-dependent; oracle/post_oracle.py's fog
+// takes either cube (tests/test_post_effects.py compares both).
+__device__ __forceinline__ float cube_rn(float a) {
+  const double d = (double)a;
+  return (float)((d * d) * d);
 }
 
 // post_processor.py:451-493 (Fog): fog colour pure white, fog_start from the parameters.
@@ -97,7 +114,7 @@ __global__ void __launch_bounds__(256) fog_kernel(const uint8_t* __restrict__ im
   if (dmax > 1.0f) dn = dn / dmax;
   float a = fmaxf(dn - start_f, 0.0f) / denom_f;
   a = fminf(fmaxf(a, 0.0f), 1.0f);
-  a = powf(a, 3.0f);
+  a = cube_rn(a);
   a = a * 0.3f;
   const float keep = 1.0f - a;
 #pragma unroll
@@ -302,9 +319,9 @@ int nerf_effect_fog(const uint8_t* image, const float* depth, int64_t depth_stri
   return check_launch("fog_kernel");
 }
 
-int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W, int levels,
+int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W, double levels,
                      double edge_strength, uint8_t* out, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
-  EREQUIRE(H > 0 && W > 0 && depth_stride >= 1 && levels > 0, "nerf_effect_toon: H=%d W=%d stride=%lld levels=%d",
+  EREQUIRE(H > 0 && W > 0 && depth_stride >= 1 && levels > 0.0, "nerf_effect_toon: H=%d W=%d stride=%lld levels=%g",
            H, W, (long long)depth_stride, levels);
   EREQUIRE(image && out && workspace && ws_bytes >= nerf_effect_workspace_bytes(H, W),
            "nerf_effect_toon: null pointer or workspace too small");

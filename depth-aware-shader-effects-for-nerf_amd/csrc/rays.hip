@@ -111,6 +111,21 @@ int launch_stratified(const float* o, const float* d, int64_t B, float near_f, f
   return check_launch("stratified_kernel");
 }
 
+// The in-kernel generator itself: out[i] = hash_uniform(seed, first + i), the uniform the
+// stratified jitter (key = seed) and the inverse-CDF draw (key = seed ^ 0x5DEECE66D) use at
+// counter first + i.  Exposed so its distribution can be tested (tests/test_gpu_rng.py).
+__global__ void __launch_bounds__(256) rng_uniforms_kernel(uint64_t seed, int64_t first, int64_t n,
+                                                           float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = hash_uniform(seed, (uint64_t)(first + i));
+}
+
+int launch_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, hipStream_t s) {
+  if (n == 0) return NERF_OK;
+  hipLaunchKernelGGL(rng_uniforms_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seed, first, n, out);
+  return check_launch("rng_uniforms_kernel");
+}
+
 // ----------------------------------------------------------------- positional encoding
 // PositionalEncoding.__call__ (src/models.py:14-47): out = [x, sin(2^0 x), cos(2^0 x), ...,
 // sin(2^(L-1) x), cos(2^(L-1) x)] along the last dim (x dropped when include_input is 0).

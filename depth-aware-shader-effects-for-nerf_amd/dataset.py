@@ -28,7 +28,7 @@ SYNTHETIC_RADIUS = 4.031128857175383     # |t| of the Blender nerf_synthetic tra
 
 
 class _RayBatches:
-    """get_rays(idx=None, batch_size=None) of dataset.py:211-277 over self.c2w / self._pixels."""
+    """get_rays(idx=None, batch_size=None) of dataset.py:206-277 over self.c2w / self._pixels."""
 
     def __len__(self):
         return len(self.c2w)
@@ -37,6 +37,9 @@ class _RayBatches:
         o, d = _get_rays(self.H, self.W, self.focal, self.c2w[idx].to(_lib.device()))
         return o.reshape(-1, 3), d.reshape(-1, 3)
 
+    def _app_idx(self, idx):
+        return idx if self.use_appearance else -1                                   # dataset.py:167-170
+
     def get_rays(self, idx=None, batch_size=None):
         if batch_size is None:
             batch_size = self.config.batch_size
@@ -44,7 +47,7 @@ class _RayBatches:
             o, d = self._rays(idx)
             rgb, alpha = self._pixels(idx, None, o, d)
             return {"rays_o": o, "rays_d": d, "rgb": rgb, "alpha": alpha,
-                    "appearance_idx": idx if self.use_appearance else -1, "img_idx": idx}
+                    "appearance_idx": self._app_idx(idx), "img_idx": idx}
         img_idx = np.random.randint(0, len(self))                                   # dataset.py:250
         o, d = self._rays(img_idx)
         sel = np.random.choice(self.H * self.W, size=batch_size, replace=False)    # dataset.py:260
@@ -52,53 +55,98 @@ class _RayBatches:
         o, d = o[sel_t].contiguous(), d[sel_t].contiguous()
         rgb, alpha = self._pixels(img_idx, sel, o, d)
         return {"rays_o": o, "rays_d": d, "rgb": rgb, "alpha": alpha,
-                "appearance_idx": img_idx if self.use_appearance else -1, "img_idx": img_idx}
+                "appearance_idx": self._app_idx(img_idx), "img_idx": img_idx}
+
+    def __getitem__(self, idx):
+        """dataset.py:129-204: {'img' (3,H,W), 'alpha' (1,H,W) or None, 'c2w' (4,4),
+        'appearance_idx', 'img_idx'} on the CPU."""
+        if idx < 0:
+            idx += len(self)
+        if not 0 <= idx < len(self):
+            raise IndexError(f"image index {idx} out of range for {len(self)} images")
+        rgb, alpha = self._image_chw(idx)
+        return {"img": rgb, "alpha": alpha, "c2w": self.c2w[idx].clone(), "appearance_idx": self._app_idx(idx),
+                "img_idx": idx}
+
+
+def _appearance_table(n, dim):
+    """dataset.py:79-83: one trainable embedding per image, randn(n, dim) as an nn.Parameter."""
+    return torch.nn.Parameter(torch.randn(n, dim))
 
 
 class NeRFDataset(_RayBatches):
-    """dataset.py:9-209 for dataset_type 'nerf_synthetic'."""
+    """dataset.py:9-204: 'nerf_synthetic' scenes (transforms_<split>.json + RGBA PNGs under
+    dataset_path/scene) and the custom format (dataset_path/../transforms.json, all frames but
+    the last for 'train', the last one otherwise).  Decoded images are cached, where the
+    reference decodes a PNG on every batch (dataset.py:156,250-251)."""
 
     def __init__(self, config, split="train"):
         from PIL import Image
         self.config, self.split = config, split
-        scene_path = os.path.join(config.dataset_path, config.scene)
-        with open(os.path.join(scene_path, f"transforms_{split}.json")) as f:
-            self.meta = json.load(f)
-        self.frames = self.meta["frames"]
-        self.paths = []
-        for fr in self.frames:
-            p = fr["file_path"]
-            p = p[2:] if p.startswith("./") else p
-            self.paths.append(os.path.join(scene_path, p + ".png"))
-        with Image.open(self.paths[0]) as img:
-            self.W, self.H = img.size
-        if "camera_angle_x" in self.meta:                                          # dataset.py:65-72
-            self.focal = 0.5 * self.W / np.tan(0.5 * self.meta["camera_angle_x"])
+        self._cache = {}
+        self.dataset_type = getattr(config, "dataset_type", "nerf_synthetic")
+        if self.dataset_type == "nerf_synthetic":                                 # dataset.py:29-83
+            scene_path = os.path.join(config.dataset_path, config.scene)
+            with open(os.path.join(scene_path, f"transforms_{split}.json")) as f:
+                self.meta = json.load(f)
+            self.frames = self.meta["frames"]
+            self.paths = []
+            for fr in self.frames:
+                p = fr["file_path"]
+                p = p[2:] if p.startswith("./") else p
+                self.paths.append(os.path.join(scene_path, p + ".png"))
+            with Image.open(self.paths[0]) as img:
+                self.W, self.H = img.size
+            width = self.W
+            self.near, self.far = config.near, config.far
+        else:                                                                      # dataset.py:85-124
+            with open(os.path.join(config.dataset_path, "../transforms.json")) as f:
+                self.meta = json.load(f)
+            self.frames = self.meta["frames"][:-1] if split == "train" else self.meta["frames"][-1:]
+            self.paths = [os.path.join(config.dataset_path, fr["file_path"]) for fr in self.frames]
+            self.H, self.W = self.meta["h"], self.meta["w"]
+            width = self.meta["w"]
+            self.near, self.far = 2.0, 6.0
+        if "camera_angle_x" in self.meta:                                          # dataset.py:65-71
+            self.focal = 0.5 * width / np.tan(0.5 * self.meta["camera_angle_x"])
         elif "fl_x" in self.meta:
             self.focal = self.meta["fl_x"]
         else:
-            self.focal = self.W / (2 * np.tan(np.radians(55) / 2))
-        self.near, self.far = config.near, config.far
+            self.focal = width / (2 * np.tan(np.radians(55) / 2))
         self.use_appearance = config.use_appearance
-        self.appearance_embeddings = torch.randn(len(self.frames), config.appearance_dim) \
+        self.appearance_embeddings = _appearance_table(len(self.frames), config.appearance_dim) \
             if self.use_appearance else None
         self.c2w = [torch.tensor(fr["transform_matrix"], dtype=torch.float32) for fr in self.frames]
 
-    def _image(self, idx):
-        from PIL import Image
-        with Image.open(self.paths[idx]) as img:
-            arr = np.asarray(img, dtype=np.uint8)
-        t = torch.from_numpy(arr.astype(np.float32) / 255.0)                        # ToTensor, HWC
-        rgb = t[..., :3].reshape(-1, 3)
-        alpha = t[..., 3:4].reshape(-1, 1) if t.shape[-1] == 4 else torch.ones(rgb.shape[0], 1)
-        return rgb, alpha
+    def _image_chw(self, idx):
+        """ToTensor of the image file (dataset.py:156-161): rgb (3,H,W) in [0,1], alpha (1,H,W)
+        (ones without an alpha channel; None for the custom format, dataset.py:182,190)."""
+        if idx not in self._cache:
+            from PIL import Image
+            with Image.open(self.paths[idx]) as img:
+                if self.dataset_type != "nerf_synthetic":
+                    img = img.convert("RGB")
+                arr = np.asarray(img, dtype=np.uint8)
+            if arr.ndim == 2:
+                arr = arr[..., None]
+            t = torch.from_numpy(arr.copy()).permute(2, 0, 1).float().div(255)   # ToTensor
+            rgb = t[:3]
+            if self.dataset_type != "nerf_synthetic":
+                alpha = None
+            else:
+                alpha = t[3:4] if t.shape[0] == 4 else torch.ones_like(t[:1])
+            self._cache[idx] = (rgb, alpha)
+        return self._cache[idx]
 
     def _pixels(self, idx, sel, o, d):
-        rgb, alpha = self._image(idx)
+        rgb, alpha = self._image_chw(idx)
+        rgb = rgb.permute(1, 2, 0).reshape(-1, 3)                                   # dataset.py:235,265
+        alpha = alpha.permute(1, 2, 0).reshape(-1, 1) if alpha is not None else None
         if sel is not None:
-            rgb, alpha = rgb[sel], alpha[sel]
+            rgb = rgb[sel]
+            alpha = alpha[sel] if alpha is not None else None
         dev = o.device
-        return rgb.to(dev), alpha.to(dev)
+        return rgb.to(dev), (alpha.to(dev) if alpha is not None else None)
 
 
 class SyntheticNeRFDataset(_RayBatches):
@@ -126,7 +174,8 @@ class SyntheticNeRFDataset(_RayBatches):
             torch.manual_seed(teacher_seed)
             self.teacher = NeRF(config).to(_lib.device()).eval()
             self.teacher_app = torch.randn(n_images, config.appearance_dim, generator=g)
-        self.appearance_embeddings = torch.randn(n_images, config.appearance_dim) if self.use_appearance else None
+        self.appearance_embeddings = _appearance_table(n_images, config.appearance_dim) \
+            if self.use_appearance else None
         self.n_samples = n_samples or config.num_samples
 
     @torch.no_grad()
@@ -136,6 +185,12 @@ class SyntheticNeRFDataset(_RayBatches):
         rgb, _, _ = volume_render(self.teacher, o, d, self.near, self.far, self.n_samples, 0,
                                   appearance_embedding=app, perturb=False)
         return rgb, torch.ones(rgb.shape[0], 1, device=o.device)
+
+    def _image_chw(self, idx):
+        o, d = self._rays(idx)
+        rgb, alpha = self._pixels(idx, None, o, d)
+        return (rgb.reshape(self.H, self.W, 3).permute(2, 0, 1).cpu().contiguous(),
+                alpha.reshape(self.H, self.W, 1).permute(2, 0, 1).cpu().contiguous())
 
 
 def make_dataset(config, split="train", **synthetic_kw):

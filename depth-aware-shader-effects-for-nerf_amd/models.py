@@ -57,9 +57,37 @@ STATE_KEYS = tuple(
        "appearance_projection.weight", "appearance_projection.bias", "rgb_linear.weight", "rgb_linear.bias"])
 
 
+APP_KEYS = ("appearance_projection.weight", "appearance_projection.bias")
+_APP_SHAPES = ((128, _APP_DIM), (128,))
+
+
+def state_tensors(sd, dev=None):
+    """The 24 packer inputs in STATE_KEYS order from a state_dict.  A model built with
+    use_appearance=False has no appearance_projection (models.py:99-103); its two slots are
+    zeros, which the kernels never read because such a model ignores the embedding
+    (models.py:146)."""
+    out = []
+    for k in STATE_KEYS:
+        if k in sd:
+            out.append(sd[k])
+        elif k in APP_KEYS:
+            out.append(torch.zeros(_APP_SHAPES[APP_KEYS.index(k)], device=dev))
+        else:
+            raise KeyError(f"state_dict has no {k!r}")
+    return out
+
+
+def uses_appearance(model):
+    """models.py:146: the embedding is used only when config.use_appearance is set."""
+    cfg = getattr(model, "config", None)
+    if cfg is not None:
+        return bool(cfg.use_appearance)
+    return hasattr(model, "appearance_projection")
+
+
 def _check_config(config):
     want = dict(hidden_dim=256, num_layers=8, skip_connect_layers=[4], pos_enc_levels=10, dir_enc_levels=4,
-                use_appearance=True, appearance_dim=_APP_DIM)
+                appearance_dim=_APP_DIM)
     bad = {}
     for k, v in want.items():
         got = getattr(config, k)
@@ -90,7 +118,8 @@ class NeRF(nn.Module):
                 self.pts_linears.append(nn.Linear(config.hidden_dim, config.hidden_dim))
         self.density_head = nn.Linear(config.hidden_dim, 1)
         self.dir_linear = nn.Linear(config.hidden_dim + dir_enc_dim, config.hidden_dim // 2)
-        self.appearance_projection = nn.Linear(config.appearance_dim, config.hidden_dim // 2)
+        if config.use_appearance:                                      # models.py:99-103
+            self.appearance_projection = nn.Linear(config.appearance_dim, config.hidden_dim // 2)
         self.rgb_linear = nn.Linear(config.hidden_dim // 2, 3)
         self._packed = None
         self._packed_key = None
@@ -100,10 +129,9 @@ class NeRF(nn.Module):
         """Device buffer of the MFMA-layout weights; re-packed when any parameter changes."""
         dev = _lib.device()
         sd = self.state_dict()
-        tensors = [sd[k] for k in STATE_KEYS]
-        key = (dev,) + tuple((t.data_ptr(), t._version, t.device) for t in tensors)
+        key = (dev,) + tuple((sd[k].data_ptr(), sd[k]._version, sd[k].device) for k in STATE_KEYS if k in sd)
         if self._packed is None or self._packed_key != key:
-            self._packed = pack_params(tensors, dev)
+            self._packed = pack_params(state_tensors(sd, dev), dev)
             self._packed_key = key
         return self._packed
 
@@ -118,7 +146,7 @@ class NeRF(nn.Module):
         xs = x.reshape(-1, 3).to(dev, torch.float32).contiguous()
         ds = d.reshape(-1, 3).to(dev, torch.float32).contiguous()
         M = xs.shape[0]
-        app, rows = app_rows(appearance_embedding, M, dev)
+        app, rows = app_rows(appearance_embedding if self.config.use_appearance else None, M, dev)
         return run_mlp(self.packed_weights(), xs, ds, None, M, 1, app, rows, lead, x.device)
 
 

@@ -122,7 +122,7 @@ class PostProcessor:
         out = torch.empty_like(img)
         ws = self._workspace(H, W)
         _lib.check(_lib.load().nerf_effect_toon(_lib.ptr(img), _lib.ptr(d), 1, H, W,
-                                                int(self.params.get("toon_levels", 5)),
+                                                float(self.params.get("toon_levels", 5)),
                                                 float(self.params.get("toon_edge_strength", 1.0)), _lib.ptr(out),
                                                 _lib.ptr(ws), ws.numel(), _lib.stream()), "nerf_effect_toon")
         return out.cpu().numpy() if as_numpy else out

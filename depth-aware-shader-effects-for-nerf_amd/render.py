@@ -24,7 +24,7 @@ and ``background_color``.  Keyword-only extras:
 import torch
 
 from . import _lib
-from .models import STATE_KEYS, app_rows, pack_params, run_mlp
+from .models import STATE_KEYS, app_rows, pack_params, run_mlp, state_tensors, uses_appearance
 from .ray_utils import draw_seed, linspace_table
 
 _FOREIGN = {}
@@ -37,10 +37,9 @@ def packed_for(model):
         return model.packed_weights()
     dev = _lib.device()
     sd = model.state_dict()
-    tensors = [sd[k] for k in STATE_KEYS]
-    key = (id(model), dev) + tuple((t.data_ptr(), t._version) for t in tensors)
+    key = (id(model), dev) + tuple((sd[k].data_ptr(), sd[k]._version) for k in STATE_KEYS if k in sd)
     if _FOREIGN.get(id(model), (None,))[0] != key:
-        _FOREIGN[id(model)] = (key, pack_params(tensors, dev))
+        _FOREIGN[id(model)] = (key, pack_params(state_tensors(sd, dev), dev))
     return _FOREIGN[id(model)][1]
 
 
@@ -57,7 +56,7 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
     Nf = int(n_importance) if hierarchical else 0
     T = N + Nf
     packed = packed_for(model)
-    app, rows = app_rows(appearance_embedding, B, dev)
+    app, rows = app_rows(appearance_embedding if uses_appearance(model) else None, B, dev)
     tr = t_rand.reshape(B, N).to(dev, torch.float32).contiguous() if (perturb and t_rand is not None) else None
     ur = u_rand.reshape(B, Nf).to(dev, torch.float32).contiguous() if (Nf and u_rand is not None) else None
     if seed is None and ((perturb and tr is None) or (Nf and ur is None)):

@@ -42,7 +42,7 @@ enum nerf_status {
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* nerf_last_error(void);
-/* ABI version (bumped on any signature or layout change). */
+/* ABI version (bumped on any signature or layout change; 6: nerf_effect_toon takes double levels). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays
@@ -60,6 +60,11 @@ int nerf_normalize_dirs(const float* rays_d, int64_t B, float* out, nerf_stream_
  * (M, dims*(2*levels + include_input)) = [x, sin(2^0 x), cos(2^0 x), ...]. */
 int nerf_positional_encoding(const float* x, int64_t M, int dims, int levels, int include_input,
                              float* out, nerf_stream_t stream);
+
+/* The in-kernel uniform generator (splitmix64 finaliser of seed + golden*(i+1), top 24 bits):
+ * out[i] = u(seed, first + i).  Stratified jitter of sample s of ray r uses u(seed, r*N + s);
+ * the inverse-CDF draw j of ray r uses u(seed ^ 0x5DEECE66D, r*Nf + j) inside nerf_render_rays. */
+int nerf_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, nerf_stream_t stream);
 
 /* ------------------------------------------------------------ R2 stratified
  * sample_stratified (src/ray_utils.py:52-88).  t_vals = torch.linspace(0,1,N)
@@ -173,7 +178,8 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
  * branch).  workspace: nerf_effect_workspace_bytes(H, W) device bytes.
  *   nerf_depth_normalize   run.py:248: (d - min) / (max - min + 1e-6) over n values.
  *   nerf_effect_fog        Fog (post_processor.py:451-493): white fog, fog_start < 1.
- *   nerf_effect_toon       Toon Shader (post_processor.py:64-117): colours quantised to `levels`,
+ *   nerf_effect_toon       Toon Shader (post_processor.py:64-117): colours quantised to `levels`
+ *                          (> 0; any real value, used as float32 like the reference's numpy scalar),
  *                          depth edges (bilateral 9/75/75, Sobel, threshold 0.05, 3x3 dilation) or,
  *                          without depth, colour edges (gray Laplacian, threshold 0.1) darkened by
  *                          edge_strength.  The cv2 steps are OpenCV 4's algorithms restated. */
@@ -184,7 +190,7 @@ int nerf_effect_fog(const uint8_t* image, const float* depth, int64_t depth_stri
                     double fog_start, uint8_t* out, void* workspace, size_t ws_bytes,
                     nerf_stream_t stream);
 int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W,
-                     int levels, double edge_strength, uint8_t* out, void* workspace,
+                     double levels, double edge_strength, uint8_t* out, void* workspace,
                      size_t ws_bytes, nerf_stream_t stream);
 
 #ifdef __cplusplus

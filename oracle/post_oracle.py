@@ -26,9 +26,18 @@ def depth_normalize(depth):
     return (d - d.min()) / (d.max() - d.min() + F32(1e-6))
 
 
-def fog(image, depth=None, fog_start=0.1):
+def cube_rn(a):
+    """a**3 rounded once to float32 (a*a exact in float64, the second product rounded to float64,
+    then to float32): the cube csrc/effects.hip computes."""
+    d = np.asarray(a, np.float64)
+    return ((d * d) * d).astype(F32)
+
+
+def fog(image, depth=None, fog_start=0.1, cube="numpy"):
     """post_processor.py:451-493.  The fog colour is pure white (:455-459); density and the
-    fog colour parameters are read but unused by the reference."""
+    fog colour parameters are read but unused by the reference.  cube="numpy" is the reference's
+    `adjusted ** 3.0` (numpy's float32 SIMD pow: SVML on AVX-512 hosts, within 1 ulp of the
+    correctly rounded cube and host-dependent); cube="rn" is cube_rn, the kernel's."""
     fog_color = np.array([255, 255, 255], dtype=F32)
     if depth is None:
         result = image.astype(F32) * F32(0.05) + fog_color * F32(0.95)
@@ -40,7 +49,7 @@ def fog(image, depth=None, fog_start=0.1):
         depth_norm = depth_norm / depth_norm.max()
     adjusted = np.maximum(depth_norm - F32(fog_start), F32(0.0)) / F32(1.0 - fog_start)
     adjusted = np.clip(adjusted, F32(0.0), F32(1.0))
-    adjusted = adjusted ** F32(3.0)
+    adjusted = adjusted ** F32(3.0) if cube == "numpy" else cube_rn(adjusted)
     adjusted = adjusted * F32(0.3)
     f3 = np.stack([adjusted] * 3, axis=2)
     result = image.astype(F32) * f3 + fog_color * (F32(1.0) - f3)
@@ -133,7 +142,8 @@ def dilate3(mask):
 
 
 def toon(image, depth=None, levels=5, edge_strength=1.0):
-    """post_processor.py:64-117."""
+    """post_processor.py:64-117 (`levels` as the reference uses it: a numpy weak scalar, so
+    float32(levels), integer or not)."""
     img_float = image.astype(F32)
     img_q = np.floor(img_float / F32(255.0) * F32(levels)) / F32(levels) * F32(255.0)
     if depth is not None:

@@ -16,7 +16,9 @@ the ranks (frames.py) and rank 0 writes the images.
 --mode train runs the reference's training loop (run.py:326-347 -> src/train.py) on the nerfmi
 kernels (nerfmi.train.train_nerf; the nerf_synthetic scene when present, else the
 teacher-rendered synthetic scene), data-parallel under torchrun; --iterations overrides
-Config.num_iterations.  --use_shader / --shader NAME applies a depth-aware effect of the
+Config.num_iterations; checkpoints go to --save_dir (default 'checkpoints', the reference's
+train_nerf default, while its render mode looks for checkpoints_<scene>/ — a reference
+inconsistency kept as is).  --use_shader / --shader NAME applies a depth-aware effect of the
 reference's PostProcessor on the GPU (nerfmi.PostProcessor: "Fog", "Toon Shader", "Original") to
 each frame before it is written, with run.py:248's depth normalisation; the reference's
 interactive first-frame editor (tkinter) is not reproduced, so --shader names the effect
@@ -69,6 +71,8 @@ def parse_args(argv=None):
     p.add_argument('--chunk', type=int, default=0, help='rays per render call (0 = whole frame)')
     p.add_argument('--seed', type=int, default=0, help='seed of the in-kernel sampling RNG')
     p.add_argument('--iterations', type=int, default=None, help='training iterations (default Config)')
+    p.add_argument('--save_dir', type=str, default='checkpoints',
+                   help="training checkpoint directory (the reference's train_nerf default, train.py:13)")
     return p.parse_args(argv)
 
 
@@ -204,8 +208,8 @@ def main(argv=None):
         np.random.seed(args.seed + (dist.get_rank() if world > 1 else 0))
         dataset = make_dataset(config)
         torch.manual_seed(args.random_init or 0)
-        train_nerf(config, dataset, save_dir=f"checkpoints_{args.scene}", num_iterations=args.iterations,
-                   group=dist.group.WORLD if world > 1 else None)
+        model = train_nerf(config, dataset, save_dir=args.save_dir, num_iterations=args.iterations,   # run.py:347
+                           group=dist.group.WORLD if world > 1 else None)
         if world > 1:
             dist.destroy_process_group()
         return 0

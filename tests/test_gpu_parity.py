@@ -289,18 +289,19 @@ def test_edge_sizes(nerfmi_mod, model, ref_state, app_vec):
     assert rgb.shape == (4, 5, 3) and depth.shape == (4, 5, 1)
 
 
-def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_meta):
+def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_meta, arith):
     """800x800 hierarchical 64+128 (the bench workload): size-independent properties on every ray,
-    and oracle parity on 4096 rays sampled across the frame.
+    and accuracy on 4096 rays sampled across the frame.
 
     The fine pass is ill-conditioned in the coarse weights: the inverse CDF moves a fine sample by
     ~4x the relative change of the weights, and the 2^9 positional-encoding frequency turns that
-    into phase.  GPU and CPU coarse weights differ at ~1e-5 relative (summation order inside the
-    MLP), so a handful of rays per thousand differ by up to a few 1e-4 relative end to end
-    (test_fine_pass_conditioning shows the oracle moves the same way under a 1-ulp perturbation
-    of its own weights).  Parity is therefore asserted (a) at 1e-4 for every ray with the fine
-    samples held equal (the oracle's fine pass on the GPU's z), and (b) end to end as PSNR
-    > 80 dB, >= 99.5% of values inside 1e-4 and none beyond 1e-3 relative."""
+    into phase, so two fp32 evaluations in different summation orders (the oracle's and the GPU's)
+    differ end to end on a few rays per thousand by more than either differs from the exact
+    result's neighbourhood.  Parity is therefore asserted (a) at 1e-4 for every ray with the fine
+    samples held equal (the oracle's fine pass on the GPU's z), and (b) end to end against a
+    float64 render of the same rays: the GPU's error is no worse than the fp32 CPU oracle's own
+    in max, p99.9 and median (conftest.check_no_worse_than_cpu)."""
+    from conftest import check_no_worse_than_cpu, render_h1_f64
     from nerfmi import cameras
     c2w = cameras.frame_c2w("chair").cuda()
     o, d = nerfmi_mod.get_rays(800, 800, golden_meta["F1"]["focal"], c2w)
@@ -325,16 +326,14 @@ def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_met
     r_fix, d_fix, _ = O._pass(ref_state, pts, dn, zg, app_vec)
     close(rgb[idx], r_fix, what="fine rgb, same z")
     close(depth[idx], d_fix, what="fine depth, same z")
-    # (b) end to end
+    # (b) end to end, referenced to float64
     r_ref, d_ref, ex_ref = O.render_rays_h1(ref_state, oc, dc, 2.0, 6.0, 64, 128, app_vec, None, u[idx])
     close(ex["rgb_map_coarse"][idx], ex_ref["rgb_map_coarse"], what="coarse rgb")
-    g = rgb[idx].cpu()
-    err = (g - r_ref).abs()
-    inside = (err <= 1e-6 + 1e-4 * r_ref.abs()).float().mean()
-    psnr = -10 * torch.log10(((g - r_ref) ** 2).mean())
+    r64, d64 = render_h1_f64(ref_state, oc, dc, app_vec, u[idx])
+    check_no_worse_than_cpu(rgb[idx].cpu(), r_ref, r64, f"full frame {arith} rgb")
+    check_no_worse_than_cpu(depth[idx].cpu(), d_ref, d64, f"full frame {arith} depth")
+    psnr = -10 * torch.log10(((rgb[idx].cpu() - r_ref) ** 2).mean())
     assert float(psnr) > 80, float(psnr)
-    assert float(inside) >= 0.995, float(inside)
-    assert float((err / r_ref.abs()).max()) < 1e-3
 
 
 def test_coarse_reuse_is_bit_identical(nerfmi_mod, model, golden, app_vec):

@@ -1,8 +1,10 @@
 """Training path parity on the GPU (include/nerfmi_train.h through the C ABI) against torch autograd
 on the oracle (oracle/nerf_oracle.py, pinned to the reference by F7) — SURVEY.md §8f row 2.
 
-Tolerances: the backward is fp32 throughout (MFMA fp32, no reduced precision).  Against a float64
-autograd of the same inputs, gradients agree to ~1e-5 relative in L2; a ReLU whose
+Every test runs under both MLP arithmetics: "f32" (fp32 MFMA throughout) and the default "f16x3"
+(split-f16 forward and data gradients, bf16x6 weight gradients: fp32-level results from
+multi-part products).  Against a float64 autograd of the same inputs, gradients
+agree to ~1e-5 relative in L2; a ReLU whose
 pre-activation sits within fp32 rounding of 0 can flip its mask between fp32 and fp64 and
 perturb single entries, so per-layer checks bound the relative L2 error (2e-4) and require
 >= 99.9% of entries within rtol 1e-3 rather than demanding every entry.
@@ -199,7 +201,10 @@ def test_wgrad_generic_shapes():
     L = _lib()
     lib, dev = L.load(), L.device()
     g = torch.Generator().manual_seed(9)
-    for (M, N, K, xdiv) in [(1, 1, 1, 1), (4099, 33, 70, 1), (5000, 3, 128, 1), (3000, 128, 32, 10), (777, 5, 9, 0)]:
+    for (M, N, K, xdiv) in [(1, 1, 1, 1), (4099, 33, 70, 1), (5000, 3, 128, 1), (3000, 128, 32, 10), (777, 5, 9, 0),
+                            # the production step's shapes: 4096 rays x 64 samples = 262,144 rows
+                            (262144, 256, 256, 1), (262144, 256, 63, 1), (262144, 3, 128, 1),
+                            (262144, 128, 32, 64), (262147, 1, 256, 1)]:
         a = torch.randn(M, N + 3, generator=g)
         xr = 1 if xdiv == 0 else (M + xdiv - 1) // xdiv if xdiv > 1 else M
         x = torch.randn(xr, K + 2, generator=g)
@@ -355,3 +360,62 @@ def test_training_reduces_loss_on_teacher_scene():
         losses.append(float(tr.step(b["rays_o"], b["rays_d"], b["rgb"], b["appearance_idx"], seed=i + 1)))
     assert np.all(np.isfinite(losses))
     assert np.mean(losses[-5:]) < 0.7 * np.mean(losses[:5]), losses
+
+
+def test_production_batch_matches_oracle(ref_state, app_vec):
+    """The production step (config 5, train.py:77-92): 4096 rays x 64 samples = 262,144 MLP rows,
+    the regime where the weight gradients run as 128 XCD-grouped chunks x 4 tiles with the
+    per-launch chunk lengths and the deterministic chunk reduction.  Loss and every gradient
+    against the oracle's autograd on the same rays, jitter and target."""
+    from nerfmi import cameras, get_rays
+    tr, table = _trainer(ref_state, n_images=3)
+    focal = cameras.synthetic_focal(800)
+    g = torch.Generator().manual_seed(31)
+    c2w = cameras.frame_c2w("chair", "circle", 7, 120).float()
+    o_all, d_all = get_rays(800, 800, focal, c2w.to(tr.dev))
+    sel = torch.randperm(800 * 800, generator=g)[:4096]
+    o, d = o_all.reshape(-1, 3)[sel.to(tr.dev)], d_all.reshape(-1, 3)[sel.to(tr.dev)]
+    target = torch.rand(4096, 3, generator=g)
+    t_rand = torch.rand(4096, 64, generator=g)
+    st = {k: v.clone() for k, v in ref_state.items()}
+    loss_o, _, grads_o, _ = O.train_step(st, table.clone(), 2, o.cpu(), d.cpu(), target, 2.0, 6.0, 64, t_rand)
+    loss, _ = tr.forward_backward(o, d, target.to(tr.dev), 2, t_rand=t_rand)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o)
+    for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
+        got = tr.view(tr.grad, i).detach().cpu().numpy()
+        assert rel_l2(got, grads_o[n].numpy()) < 5e-4, (n, rel_l2(got, grads_o[n].numpy()))
+
+
+def test_no_appearance_model_trains_like_the_oracle(noapp_state):
+    """use_appearance=False (models.py:99-103): 22 parameters, no appearance table; one step's
+    gradients and Adam update against the oracle."""
+    import nerfmi
+    from nerfmi import cameras, get_rays
+    from nerfmi.train import Trainer
+    cfg = nerfmi.Config()
+    cfg.use_appearance = False
+    torch.manual_seed(0)
+    model = nerfmi.NeRF(cfg)
+    tr = Trainer(cfg, model=model)
+    assert tr.param_slots == [i for i, k in enumerate(O.STATE_KEYS) if not k.startswith("appearance_projection")]
+    c2w = cameras.frame_c2w("chair", "circle", 3, 120).float()
+    o_all, d_all = get_rays(800, 800, cameras.synthetic_focal(800), c2w.to(tr.dev))
+    g = torch.Generator().manual_seed(5)
+    sel = torch.randperm(800 * 800, generator=g)[:512].to(tr.dev)
+    o, d = o_all.reshape(-1, 3)[sel], d_all.reshape(-1, 3)[sel]
+    target = torch.rand(512, 3, generator=g)
+    t_rand = torch.rand(512, 64, generator=g)
+    st = {k: v.clone() for k, v in noapp_state.items()}
+    loss_o, _, grads_o, opt = O.train_step(st, None, 0, o.cpu(), d.cpu(), target, 2.0, 6.0, 64, t_rand)
+    loss, _ = tr.forward_backward(o, d, target.to(tr.dev), 0, t_rand=t_rand)
+    assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o)
+    for i, k in enumerate(O.STATE_KEYS):
+        if k in noapp_state:
+            got = tr.view(tr.grad, i).detach().cpu().numpy()
+            assert rel_l2(got, grads_o[k].numpy()) < 5e-4, k
+    tr.optimizer_step()
+    sd = tr.optimizer_state_dict()
+    assert len(sd["param_groups"][0]["params"]) == 22 and sorted(sd["state"]) == list(range(22))
+    for k in noapp_state:
+        _params_close(model.state_dict()[k].cpu().numpy(), st[k].detach().numpy(), 1, k, frac=0.99)

@@ -88,10 +88,11 @@ def test_render_with_shader_applies_the_effect(tmp_path):
 
 @pytest.mark.gpu
 def test_train_mode_runs_the_training_loop(tmp_path, monkeypatch):
-    """--mode train (run.py:326-347) on the synthetic scene: a few iterations, a final checkpoint."""
+    """--mode train (run.py:326-347) on the synthetic scene: a few iterations, a final checkpoint in
+    train_nerf's default directory 'checkpoints' (train.py:13; run.py:347 passes no save_dir)."""
     monkeypatch.chdir(tmp_path)
     assert cli.main(["--mode", "train", "--scene", "chair", "--iterations", "3", "--random_init", "0"]) == 0
-    files = os.listdir(tmp_path / "checkpoints_chair")
+    files = os.listdir(tmp_path / "checkpoints")
     assert any(f.endswith(".pt") for f in files), files
 
 

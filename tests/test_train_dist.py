@@ -69,3 +69,41 @@ def test_single_process_sync_is_identity():
     g = torch.arange(10.0)
     average_gradients(g, None)
     assert torch.equal(g, torch.arange(10.0))
+
+
+def _worker_broadcast(rank, world, port, out):
+    """Ranks built from different seeds (as ranks that load different checkpoints or reach the
+    constructor with different RNG states would): after broadcast_state every rank holds rank 0's
+    flat buffer, and one averaged-gradient Adam step keeps them identical."""
+    from nerfmi.train import broadcast_state
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(100 + rank)
+        flat = torch.randn(1000)
+        broadcast_state([flat], dist.group.WORLD)
+        p = torch.nn.Parameter(flat.clone())
+        opt = torch.optim.Adam([p], lr=1e-3)
+        g = torch.randn(1000)              # each rank's own (different) gradient
+        average_gradients(g, dist.group.WORLD)
+        p.grad = g
+        opt.step()
+        torch.save(p.detach(), f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_ranks_start_from_rank0_and_stay_identical(tmp_path):
+    out = str(tmp_path / "p")
+    mp.spawn(_worker_broadcast, args=(2, _free_port(), out), nprocs=2, join=True)
+    p0, p1 = torch.load(out + ".0", weights_only=True), torch.load(out + ".1", weights_only=True)
+    assert torch.equal(p0, p1)
+    torch.manual_seed(100)
+    start = torch.randn(1000)
+    assert not torch.equal(p0, start) and (p0 - start).abs().max() <= 1.01e-3
+
+
+def test_step_seeds_differ_per_rank_and_step():
+    from nerfmi.train import step_seed
+    seeds = {step_seed(i, r) for i in range(1, 50) for r in range(8)}
+    assert len(seeds) == 49 * 8
