@@ -35,6 +35,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
 
+// expf rounded once: exp evaluated in double, then rounded to float.  The alpha of the
+// composite, 1 - exp(-sigma*dist), cancels catastrophically for small sigma*dist, so the
+// rounding of exp dominates the error of the coarse weights (and, through the ill-conditioned
+// inverse CDF, of the fine pass); the device's single-precision expf is a 1-ulp function, torch's
+// CPU exp is correctly rounded on almost every input.  This keeps the reference's fp32
+// expression (one float exp, then the float subtraction) with the best-rounded exp.
+__device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
+
 // Counter-based uniform in [0,1) (splitmix64 finaliser), used when the caller
 // passes no explicit uniforms; it is a device RNG for throughput runs only.
 __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {

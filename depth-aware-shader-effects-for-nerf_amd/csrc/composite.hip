@@ -45,7 +45,7 @@ composite_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma,
     if (valid) {
       z = zv[base + s];
       const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
-      alpha = 1.0f - expf(-sigma[base + s] * dist);
+      alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
       f = (double)((1.0f - alpha) + 1e-10f);
     }
     double incl = f;

@@ -332,7 +332,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float v = pr[c] + __shfl_xor(pr[c], 32) + packed[kOffRgbB + c];
-    out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
+    out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
   }
   if (h == 0 && s0 + (lane & 31) < M) {
     const int64_t o_s = out_slot ? r * out_T + out_slot[s] : s;

@@ -675,7 +675,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
-    out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
+    out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
   }
   if constexpr (SAVE) {
     if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d

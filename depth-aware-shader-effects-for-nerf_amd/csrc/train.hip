@@ -65,7 +65,7 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
     if (s < N) {
       const float z = zv[base + s];
       const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
-      const float alpha = 1.0f - expf(-sigma[base + s] * dist);
+      const float alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
       f = (double)((1.0f - alpha) + 1e-10f);
     }
     double incl = f;
@@ -88,7 +88,7 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
       const float z = zv[base + s];
       dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
       sg = sigma[base + s];
-      e = expf(-sg * dist);
+      e = expf_rn(-sg * dist);
       alpha = 1.0f - e;
       fs = (1.0f - alpha) + 1e-10f;
       f = (double)fs;

@@ -42,8 +42,8 @@ def arith(request):
 def trained_state():
     """Student weights after 200 Trainer steps (1024 rays) on the teacher-rendered scene; trained
     once under the default arithmetic so both arithmetics are checked on the same weights."""
-    if "trained" in _F64_CACHE:
-        return _F64_CACHE["trained"]
+    if "trained_state" in _F64_CACHE:
+        return _F64_CACHE["trained_state"]
     import nerfmi
     from nerfmi import _lib as L
     from nerfmi.dataset import SyntheticNeRFDataset
@@ -64,7 +64,7 @@ def trained_state():
         app = tr.appearance_embeddings[0].detach().cpu().clone()
     finally:
         L.set_mlp_arith(prev)
-    _F64_CACHE["trained"] = (st, app)
+    _F64_CACHE["trained_state"] = (st, app)
     return st, app
 
 
@@ -72,7 +72,7 @@ def adversarial_state(ref_state):
     st = {}
     for k, v in ref_state.items():
         v = v.clone()
-        if k.endswith(".weight") and v.shape[0] > 1:
+        if k.endswith(".weight") and v.shape[0] > 5:
             v[::8] *= 16.0
             v[5] *= 128.0
         elif k.endswith(".weight"):
@@ -122,6 +122,7 @@ def test_forward(which, ref_state, app_vec, trained_state, arith):
 
 
 def _render_f64(key, st, o, d, app, u):
+    key = "f64/" + key
     if key not in _F64_CACHE:
         _F64_CACHE[key] = render_h1_f64(st, o, d, app, u)
     return _F64_CACHE[key]

@@ -218,8 +218,19 @@ def test_wgrad_generic_shapes():
             L.check(lib.nerf_wgrad(L.ptr(ag), N + 3, N, L.ptr(xg), K + 2, K, xdiv, M, L.ptr(ow), L.ptr(ob), acc,
                                    L.ptr(ws), ws.numel(), L.stream()), "wgrad")
         torch.cuda.synchronize()
-        np.testing.assert_allclose(ow.cpu().numpy(), 2 * exp_w, rtol=1e-4, atol=1e-3)
-        np.testing.assert_allclose(ob.cpu().numpy(), 2 * exp_b, rtol=1e-4, atol=1e-3)
+        if M < 100000:
+            np.testing.assert_allclose(ow.cpu().numpy(), 2 * exp_w, rtol=1e-4, atol=1e-3)
+            np.testing.assert_allclose(ob.cpu().numpy(), 2 * exp_b, rtol=1e-4, atol=1e-3)
+        else:
+            # sums of 262K products: entries near 0 by cancellation have no relative accuracy in
+            # any fp32 order; bound the error against float64 by the CPU fp32 GEMM's own
+            cpu = (a[:, :N].T @ x[idx, :K]).double().numpy()
+            for got, exp, name in ((ow.cpu().numpy() / 2, exp_w, "w"), (ob.cpu().numpy() / 2, exp_b, "b")):
+                scale = np.abs(exp).max()
+                err = np.abs(got - exp).max() / scale
+                err_cpu = np.abs(cpu - exp_w).max() / np.abs(exp_w).max() if name == "w" else 0.0
+                assert err <= max(4 * err_cpu, 2e-6), (M, N, K, name, err, err_cpu)
+                assert rel_l2(got, exp) < 1e-6, (M, N, K, name, rel_l2(got, exp))
 
 
 def test_adam_matches_torch():
