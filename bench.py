@@ -1,23 +1,26 @@
 """Benchmark: rays/s of the hierarchical render path at 800x800, 64 coarse + 128 fine samples.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong] [--scene chair|hotdog]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-One step = render one 800x800 frame (640,000 rays) per GPU: get_rays -> render_rays
-(hierarchical H1: coarse 64, inverse-CDF 128, fine composite over the 192 merged samples, the
-64 coarse evaluations reused bit-identically so the fine MLP evaluates 128) with in-kernel
-stratified / inverse-CDF RNG, on a random-init NeRF of the reference architecture
-(torch.manual_seed(0); NeRF(Config())).  The rays of N frames of the run.py circle
-path are sharded contiguously over the N ranks (frames.py: rank r renders frame r, weak
-scaling, 640,000 rays per GPU) and reassembled on every rank with one RCCL all-gather of
-[r,g,b,depth] per ray.
+One step = get_rays -> render_rays (hierarchical H1: coarse 64, inverse-CDF 128, fine composite
+over the 192 merged samples, the 64 coarse evaluations reused bit-identically so the fine MLP
+evaluates 128) with in-kernel stratified / inverse-CDF RNG, on a random-init NeRF of the
+reference architecture (torch.manual_seed(0); NeRF(Config())), through the shipped path: one
+nerf_render_rays C call per rank per step (frames.render_path_frames).  The rays of the step's
+frames (run.py circle path) are sharded contiguously over the N ranks and reassembled on every
+rank with one RCCL all-gather of [r,g,b,depth] per ray (frames.py).
+  --scaling weak (default): N frames per step, rank r renders frame r (640,000 rays per GPU).
+  --scaling strong: one frame per step sharded over the N ranks (BASELINE config 4 with
+                    --scene hotdog: one 800x800 frame ray-chunk sharded across the GPUs).
 Rank 0 prints one JSON line.  value = rays of all ranks / max-over-ranks wall time.
 
 roofline: the dominant kernel is the fused PE->MLP kernel.  Its algorithmic work is 1,048,832
 FLOP per evaluated sample; each step launches it twice (B*64 and B*128
-samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, the time
-measured with HIP events around every launch inside the timed steps (on the stream it runs
-on).  --arith selects the MLP arithmetic (include/nerfmi.h, nerf_arith), both fp32-accurate:
+samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, the time measured
+live in the timed steps by HIP events the library records on the launch's own stream around each
+MLP launch inside nerf_render_rays (nerf_profile_mlp_begin/_end; no change to what runs).
+--arith selects the MLP arithmetic (include/nerfmi.h, nerf_arith), both fp32-accurate:
   f16x3 (default, mlp16_kernel): every fp32 product is three f16 MFMA products of a hi/lo split;
         peak = the f16 dense MFMA peak / 3 = 2516.8 / 3 = 838.9 TFLOP/s of fp32-equivalent work
         (MI355X_MICROARCH.md: f16 = 16x the f32 MFMA rate); "mfma_busy" reports the issued f16
@@ -26,7 +29,8 @@ on).  --arith selects the MLP arithmetic (include/nerfmi.h, nerf_arith), both fp
 cpu_baseline: the oracle (PyTorch-CPU restatement, oracle/nerf_oracle.py) timed on a
 bounded sample of the same workload on this host's cores (rank 0, N=1 only); the GPU renders
 the same rays with the same uniforms and the line reports the PSNR of its rgb against the
-oracle's (the metric's "PSNR vs reference").
+oracle's (the metric's "PSNR vs reference").  The oracle evaluates all 256 MLP points per ray
+(the reference's formulation) where the GPU evaluates 192 (coarse reuse, bit-identical).
 traffic: HBM bytes per MLP launch from the rocprofv3 PMC passes of scripts/profile_pmc.sh
 (FETCH_SIZE doubled per MI355X_MICROARCH.md + WRITE_SIZE), read from the newest
 profiles/r*_pmc_summary.json when present (PMC counters cannot be read inside this process).
@@ -59,6 +63,8 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--scene", default="chair")
+    p.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                   help="weak: one frame per rank per step; strong: one frame per step over all ranks")
     p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="MLP MFMA arithmetic")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
@@ -112,6 +118,15 @@ def pmc_traffic(arith):
     return js.get("mlp_hbm_bytes_per_launch"), os.path.relpath(paths[-1], REPO)
 
 
+def workload(scene, world, scaling):
+    """Poses of one step: weak = one circle-path frame per rank (frame k on rank k), strong = one
+    frame for all ranks.  frames.render_path_frames shards the poses' rays contiguously over the
+    ranks either way (tests/test_frames_dist.py runs this plan through gloo)."""
+    from nerfmi import cameras
+    n = world if scaling == "weak" else 1
+    return [cameras.frame_c2w(scene, "circle", frame=k % 120, num_frames=120) for k in range(n)]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,7 +136,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import nerfmi
-    from nerfmi import cameras, frames
+    from nerfmi import _lib, cameras, frames
     nerfmi.set_mlp_arith(args.arith)
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -130,14 +145,12 @@ def main():
     torch.manual_seed(1)
     app = torch.randn(100, 32)[0].to(dev)
     focal = cameras.synthetic_focal(W)
-    # one frame of the run.py circle path per rank: world x 640,000 rays per step, ray-sharded
-    poses = [cameras.frame_c2w(args.scene, "circle", frame=k % 120, num_frames=120) for k in range(world)]
+    poses = workload(args.scene, world, args.scaling)
     B = H * W
 
-    def step(i, timing=None):
+    def step(i):
         rgb, depth = frames.render_path_frames(model, poses, H, W, focal, 2.0, 6.0, N_COARSE, N_FINE,
-                                               appearance_embedding=app, perturb=True, hierarchical=True, seed=i,
-                                               timing=timing)
+                                               appearance_embedding=app, perturb=True, hierarchical=True, seed=i)
         return rgb
 
     for i in range(args.warmup):
@@ -145,36 +158,41 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timing = []
+    cap = 4 * args.steps + 8
     torch.cuda.synchronize()
+    _lib.profile_mlp_begin(cap)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, timing)
+        step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    launches = _lib.profile_mlp_end(cap)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in timing)
-    mlp_samples = sum(n for _, _, n in timing)
-    achieved = mlp_samples * FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12
+    mlp_ms = sum(ms for ms, _ in launches)
+    mlp_samples = sum(n for _, n in launches)
+    achieved = mlp_samples * FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 if mlp_ms else 0.0
+    rays_per_rank = B * len(poses) // world
     per_kind = {}
-    for a, b, n in timing:
-        k = "coarse" if n == B * N_COARSE else "fine"
-        per_kind.setdefault(k, []).append(a.elapsed_time(b))
+    for ms, n in launches:
+        per_kind.setdefault("coarse" if n == rays_per_rank * N_COARSE else "fine", []).append(ms)
     if rank == 0:
-        total_rays = B * world * args.steps
+        total_rays = B * len(poses) * args.steps
         traffic, traffic_src = pmc_traffic(args.arith)
         if args.arith == "f16x3":
             kernel, peak = "nerf::mlp16_kernel", MFMA_F16_PEAK_TFLOPS / 3
             busy = mlp_samples * F16X3_ISSUED_FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS
+            dtype = "fp32 (f16x3 split)"
         else:
             kernel, peak = "nerf::mlp_kernel", MFMA_F32_PEAK_TFLOPS
             busy = achieved / MFMA_F32_PEAK_TFLOPS
+            dtype = "fp32"
+        per_gpu = "one frame per GPU" if args.scaling == "weak" else f"one frame sharded over {world} GPU(s)"
         line = {
             "metric": "rays/sec at 800x800, 64 coarse + 128 fine samples",
             "value": total_rays / elapsed,
@@ -184,24 +202,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic: run.py circle-path poses (one frame per rank), random-init NeRF "
+            "dtype": dtype,
+            "data": "synthetic: run.py circle-path poses, random-init NeRF "
                     "(torch.manual_seed(0); NeRF(Config())), no dataset/checkpoint in the environment",
-            "config": {"workload": f"{args.scene} 800x800 frame per GPU, hierarchical {N_COARSE} coarse + "
+            "config": {"workload": f"{args.scene} 800x800, {per_gpu} per step, hierarchical {N_COARSE} coarse + "
                                    f"{N_FINE} fine (H1; fine composite over 192 merged samples, coarse "
-                                   f"evaluations reused), perturb=True",
-                       "rays_per_gpu_per_step": B, "n_coarse": N_COARSE, "n_fine": N_FINE,
-                       "mlp_evals_per_ray": N_COARSE + N_FINE,
-                       "parallelism": f"ray-shard x{world} (one frame per GPU) + RCCL all-gather"},
+                                   f"evaluations reused), perturb=True, one nerf_render_rays call per rank",
+                       "rays_per_step": B * len(poses), "rays_per_gpu_per_step": rays_per_rank,
+                       "n_coarse": N_COARSE, "n_fine": N_FINE, "mlp_evals_per_ray": N_COARSE + N_FINE,
+                       "parallelism": f"ray-shard x{world} + RCCL all-gather"},
             "mlp_arith": args.arith,
             "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "mfma_busy": busy,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                         "launches": len(timing), "avg_launch_ms": mlp_ms / max(len(timing), 1),
+                         "launches": len(launches), "avg_launch_ms": mlp_ms / max(len(launches), 1),
                          "avg_launch_ms_by_pass": {k: sum(v) / len(v) for k, v in per_kind.items()},
-                         "flop_per_sample": FLOP_PER_SAMPLE},
+                         "flop_per_sample": FLOP_PER_SAMPLE,
+                         "timing": "HIP events recorded by libnerfmi on the MLP's stream inside the timed steps"},
             "cpu_baseline": None,
             "psnr_vs_reference_db": None,
         }

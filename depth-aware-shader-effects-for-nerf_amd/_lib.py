@@ -38,6 +38,8 @@ _SIGNATURES = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nerf_profile_mlp_begin": (ctypes.c_int, [ctypes.c_int]),
+    "nerf_profile_mlp_end": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "nerf_rng_uniforms": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_void_p]),
     "nerf_packed_weights_floats": (ctypes.c_size_t, []),
@@ -156,3 +158,19 @@ def stream():
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def profile_mlp_begin(capacity=4096):
+    """Start bracketing every fused-MLP launch with HIP events on its stream (bench.py roofline)."""
+    check(load().nerf_profile_mlp_begin(int(capacity)), "nerf_profile_mlp_begin")
+    return int(capacity)
+
+
+def profile_mlp_end(capacity=4096):
+    """Stop recording; [(ms, samples)] per MLP launch since profile_mlp_begin."""
+    ms = (ctypes.c_float * capacity)()
+    samples = (ctypes.c_int64 * capacity)()
+    count = ctypes.c_int(0)
+    check(load().nerf_profile_mlp_end(ms, samples, capacity, ctypes.byref(count)), "nerf_profile_mlp_end")
+    n = min(count.value, capacity)
+    return [(float(ms[i]), int(samples[i])) for i in range(n)]

@@ -6,6 +6,8 @@
 #include <stdarg.h>
 #include <string.h>
 
+#include <vector>
+
 #include "common.h"
 
 namespace nerf {
@@ -298,6 +300,61 @@ int nerf_ray_features(const float* packed, const float* dirs, int64_t R, const f
   return launch_ray_features(packed, dirs, R, app, app_rows, feat, (hipStream_t)stream);
 }
 
+// ------------------------------------------------------------------ MLP launch profiling
+// bench.py's roofline leg: while on, every fused-MLP launch (nerf_render_rays' two, or
+// nerf_mlp_forward's one) is bracketed by HIP events recorded on the launch's own stream, so the
+// shipped single-call path is timed per launch with no change to what it runs.  One process-wide
+// recorder (a diagnostic for one host thread).
+namespace {
+struct MlpProfile {
+  std::vector<hipEvent_t> ev;
+  std::vector<int64_t> samples;
+  int n = 0;
+  bool on = false;
+};
+MlpProfile g_prof;
+}  // namespace
+
+static int profiled_mlp(const float* packed, const float* origins, const float* dirs, const float* z, int64_t R,
+                        int N, const float* feat, float* rgb, float* sigma, const int* slot, int T, hipStream_t s) {
+  const bool rec = g_prof.on && g_prof.n < (int)g_prof.samples.size();
+  if (rec && hipEventRecord(g_prof.ev[2 * g_prof.n], s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "nerf profile: hipEventRecord failed");
+  if (int rc = launch_mlp(packed, origins, dirs, z, R, N, feat, rgb, sigma, slot, T, s)) return rc;
+  if (rec) {
+    if (hipEventRecord(g_prof.ev[2 * g_prof.n + 1], s) != hipSuccess)
+      return set_error(NERF_ERR_HIP, "nerf profile: hipEventRecord failed");
+    g_prof.samples[g_prof.n++] = R * (int64_t)N;
+  }
+  return NERF_OK;
+}
+
+int nerf_profile_mlp_begin(int capacity) {
+  REQUIRE(capacity >= 1 && capacity <= 1 << 20, "nerf_profile_mlp_begin: capacity=%d", capacity);
+  for (hipEvent_t e : g_prof.ev) hipEventDestroy(e);
+  g_prof.ev.assign(2 * (size_t)capacity, nullptr);
+  for (auto& e : g_prof.ev)
+    if (hipEventCreate(&e) != hipSuccess) return set_error(NERF_ERR_HIP, "nerf_profile_mlp_begin: hipEventCreate failed");
+  g_prof.samples.assign(capacity, 0);
+  g_prof.n = 0;
+  g_prof.on = true;
+  return NERF_OK;
+}
+
+int nerf_profile_mlp_end(float* ms, int64_t* samples, int capacity, int* count) {
+  REQUIRE(count && (capacity == 0 || (ms && samples)), "nerf_profile_mlp_end: null pointer");
+  g_prof.on = false;
+  const int n = g_prof.n < capacity ? g_prof.n : capacity;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(g_prof.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms[i], g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess)
+      return set_error(NERF_ERR_HIP, "nerf_profile_mlp_end: event %d", i);
+    samples[i] = g_prof.samples[i];
+  }
+  *count = g_prof.n;
+  return NERF_OK;
+}
+
 int nerf_mlp_forward(const float* packed, const float* origins, const float* dirs, const float* z_vals, int64_t R,
                      int N, const float* ray_feat, float* rgb, float* sigma, const int32_t* out_slot, int out_T,
                      nerf_stream_t stream) {
@@ -306,7 +363,7 @@ int nerf_mlp_forward(const float* packed, const float* origins, const float* dir
   REQUIRE(z_vals || N == 1, "nerf_mlp_forward: without z_vals the origins are the points and N must be 1");
   REQUIRE(R == 0 || (packed && origins && ray_feat && rgb && sigma && (!z_vals || dirs)),
           "nerf_mlp_forward: null pointer");
-  return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, out_slot, out_T, (hipStream_t)stream);
+  return profiled_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, out_slot, out_T, (hipStream_t)stream);
 }
 
 int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, int64_t B, int N, float* rgb_map,
@@ -375,7 +432,7 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
                               z, nullptr, s)))
     return rc;                                                                                 // render.py:22
   if ((rc = launch_ray_features(packed, dn, B, app, app_rows, feat, s))) return rc;
-  if ((rc = launch_mlp(packed, rays_o, dn, z, B, N, feat, rgb_c, sigma_c, nullptr, 0, s))) return rc;  // :49
+  if ((rc = profiled_mlp(packed, rays_o, dn, z, B, N, feat, rgb_c, sigma_c, nullptr, 0, s))) return rc;  // :49
   if (Nf == 0)
     return launch_composite(rgb_c, sigma_c, z, B, N, rgb_map, depth_map, wc, s);               // render.py:56-80
   float* crgb = coarse_rgb ? coarse_rgb : maps;
@@ -391,7 +448,7 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed ^ 0x5DEECE66Dull, z_all,
                               nullptr, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, slot, s)))
     return rc;
-  if ((rc = launch_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_all, sigma_all, slot, T, s))) return rc;
+  if ((rc = profiled_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_all, sigma_all, slot, T, s))) return rc;
   return launch_composite(rgb_all, sigma_all, z_all, B, T, rgb_map, depth_map, weights_out, s);
 }
 

@@ -66,6 +66,14 @@ int nerf_positional_encoding(const float* x, int64_t M, int dims, int levels, in
  * the inverse-CDF draw j of ray r uses u(seed ^ 0x5DEECE66D, r*Nf + j) inside nerf_render_rays. */
 int nerf_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, nerf_stream_t stream);
 
+/* Per-launch timing of the fused MLP (bench.py's roofline): after nerf_profile_mlp_begin(cap),
+ * each MLP launch inside nerf_render_rays / nerf_mlp_forward (up to cap) is bracketed by HIP
+ * events on its own stream; nerf_profile_mlp_end synchronises them and writes each launch's
+ * milliseconds and sample count (min(recorded, capacity) entries; *count = launches recorded)
+ * and stops recording.  Process-wide; for one host thread. */
+int nerf_profile_mlp_begin(int capacity);
+int nerf_profile_mlp_end(float* ms, int64_t* samples, int capacity, int* count);
+
 /* ------------------------------------------------------------ R2 stratified
  * sample_stratified (src/ray_utils.py:52-88).  t_vals = torch.linspace(0,1,N)
  * (N floats, device).  perturb: t_rand (B,N) uniforms when non-null, else an

@@ -96,3 +96,34 @@ def test_world2_reassembles_the_single_process_frames(tmp_path):
     # the oracle's CPU GEMM blocks differently for 30- and 60-ray batches: equal to rounding
     assert torch.allclose(got["rgb1"].reshape(-1, 3), r_ref, rtol=1e-5, atol=1e-7)
     assert torch.allclose(got["depth1"].reshape(-1), d_ref[:, 0], rtol=1e-5, atol=1e-7)
+
+
+def _worker_bench(rank, world, port, out):
+    """bench.py's own step plan (bench.workload) through frames.render_frames_sharded, both
+    scaling modes, at world 2 over gloo."""
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        for scaling in ("weak", "strong"):
+            ps = bench.workload("hotdog", world, scaling)
+            res[scaling] = frames.render_frames_sharded(ray_fn_for(ps, 7.5), fake_render, H, W, len(ps))
+        if rank == 0:
+            torch.save(res, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_plans_world2(tmp_path):
+    """Strong scaling (BASELINE config 4: one hotdog frame sharded over the ranks) and weak
+    scaling (one frame per rank) reassemble exactly the single-process frames."""
+    import bench
+    assert len(bench.workload("hotdog", 2, "strong")) == 1 and len(bench.workload("hotdog", 2, "weak")) == 2
+    out = str(tmp_path / "bench.pt")
+    mp.spawn(_worker_bench, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for scaling in ("weak", "strong"):
+        ps = bench.workload("hotdog", 2, scaling)
+        ref = frames.render_frames_sharded(ray_fn_for(ps, 7.5), fake_render, H, W, len(ps))
+        assert torch.equal(got[scaling][0], ref[0]) and torch.equal(got[scaling][1], ref[1]), scaling
