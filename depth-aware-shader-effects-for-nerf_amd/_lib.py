@@ -14,6 +14,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NERFMI_LIB") or os.path.join(_PKG_DIR, "libnerfmi.so")
 
 _c_float_p = ctypes.c_void_p  # device pointers travel as integers
+SAVE_ROW, GRAD_ROW, MASK_ROW = 2400, 2312, 68   # include/nerfmi_train.h NERF_SAVE_ROW, _GRAD_ROW, _MASK_ROW
 _V, _I64 = ctypes.c_void_p, ctypes.c_int64
 
 # name -> (restype, argtypes)
@@ -69,10 +70,10 @@ _SIGNATURES = {
                                                     ctypes.c_void_p]),
     "nerf_pack_weights_transposed_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "nerf_ray_features_train": (ctypes.c_int, [_V, _V, _I64, _V, _I64, _V, _V, _V]),
-    "nerf_mlp_forward_train": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V, _V, _V, _V]),
+    "nerf_mlp_forward_train": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V, _V, _V, _V, _V]),
     "nerf_composite_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, ctypes.c_int, ctypes.c_float, _V, _V, _V,
                                                _V]),
-    "nerf_mlp_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _I64, _V, _V]),
+    "nerf_mlp_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _V, _V]),
     "nerf_param_grads_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "nerf_param_grads": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, _V, _I64, _V, ctypes.POINTER(ctypes.c_void_p),
                                         _V, _V, ctypes.c_size_t, _V]),
@@ -97,7 +98,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 

@@ -197,7 +197,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 6; }
+int nerf_abi_version(void) { return 7; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -331,7 +331,7 @@ static int profiled_mlp(const float* packed, const float* origins, const float* 
 
 int nerf_profile_mlp_begin(int capacity) {
   REQUIRE(capacity >= 1 && capacity <= 1 << 20, "nerf_profile_mlp_begin: capacity=%d", capacity);
-  for (hipEvent_t e : g_prof.ev) hipEventDestroy(e);
+  for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
   g_prof.ev.assign(2 * (size_t)capacity, nullptr);
   for (auto& e : g_prof.ev)
     if (hipEventCreate(&e) != hipSuccess) return set_error(NERF_ERR_HIP, "nerf_profile_mlp_begin: hipEventCreate failed");

@@ -72,10 +72,10 @@ int launch_ray_features(const float* packed, const float* dirs, int64_t R, const
 extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
-                 float* save = nullptr, const float* encd = nullptr);
+                 float* save = nullptr, const float* encd = nullptr, uint32_t* masks = nullptr);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
                int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
-               hipStream_t s, float* save = nullptr, const float* encd = nullptr);
+               hipStream_t s, float* save = nullptr, const float* encd = nullptr, uint32_t* masks = nullptr);
 int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N,
                      float* rgb_map, float* depth, float* weights, hipStream_t s);
 

@@ -146,12 +146,8 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
     static_for<4>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       constexpr int g = 4 * st + i;
-#ifndef NERF_MLP_NOLOAD
       if constexpr (g + DEPTH < G) ring[g % DEPTH] = wf[stream_block<NT, KSQ>(g + DEPTH) * 64];
       else ring[g % DEPTH] = nf[(((g + DEPTH - G) % 4) * next_ksq + (g + DEPTH - G) / 4) * 64];
-#else   // timing-only build: the weight stream removed (wrong results)
-      asm volatile("" : "+v"(ring[g % DEPTH]));
-#endif
     });
     // keep the ring's issue order: without this the scheduler hoists the layer's weight
     // loads and runs out of registers
@@ -215,12 +211,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       float sn, cs;
-#ifndef NERF_MLP_NOPE
       sincosf(x[c] * (float)(1 << i), &sn, &cs);
-#else   // timing-only build: PE without the transcendental (wrong results)
-      sn = x[c] * (float)(1 << i);
-      cs = sn + 1.0f;
-#endif
       pe[3 * i + c] = h ? cs : sn;
     }
   }
@@ -345,11 +336,11 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
-               float* save, const float* encd) {
+               float* save, const float* encd, uint32_t* masks) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3)
-    return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s, save, encd);
+    return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s, save, encd, masks);
   constexpr int per_block = 32 * NERF_MLP_WAVES;
   const int64_t blocks = (M + per_block - 1) / per_block;
   if (save)

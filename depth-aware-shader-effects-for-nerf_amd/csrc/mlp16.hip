@@ -112,9 +112,6 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
                                                 uint32_t voff) {
-#ifdef NERF16_T_NODMA
-  return;
-#endif
   const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
 #ifdef NERF16_M0_SAVE
   uint32_t keep;
@@ -155,11 +152,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 // A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
 template <int KK>
 __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
-#ifdef NERF16_T_NOREAD
-#pragma unroll
-  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
-  return;
-#endif
 #pragma unroll
   for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
@@ -171,11 +163,6 @@ __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], 
 // One k-step of group G (tiles 4G .. 4G+3).
 template <int G, bool FIRST, typename Hook>
 __device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8], Hook&& hook) {
-#ifdef NERF16_T_NOMFMA   // timing-only builds (scripts/microbench/mlp16_stamps.hip); wrong results
-#pragma unroll
-  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[4 * G + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
-  return;
-#endif
   static_for<4>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     f32x16 c;
@@ -202,10 +189,18 @@ __device__ __forceinline__ constexpr int side_quarters(int hs) {
 }
 // Training forward (SAVE): global stores of ReLU(y) (one f32x4 per converted quarter) issued in
 // half-step hs; they count in vmcnt with the stream's DMA (skip-layer PE operands store nothing).
+// Plus the ReLU-mask store of each tile, issued with the tile's last quarter (QG % 4 == 3).
+template <int KIND>
+__device__ __forceinline__ constexpr int side_mask_stores(int hs) {
+  if constexpr (KIND == kSidePrev || KIND == kSideSkipPrev) return (hs == 2 || hs == 6 || hs == 10 || hs == 14) ? 1 : 0;
+  if constexpr (KIND == kSideCur) return (hs == 4 || hs == 8 || hs == 12 || hs == 15) ? 1 : 0;
+  if constexpr (KIND == kSideL0) return 1;
+  return 0;
+}
 template <int KIND>
 __device__ __forceinline__ constexpr int side_stores(int hs) {
-  if constexpr (KIND == kSideSkipPrev) return side_quarters<kSidePrev>(hs);
-  return side_quarters<KIND>(hs);
+  if constexpr (KIND == kSideSkipPrev) return side_quarters<kSidePrev>(hs) + side_mask_stores<KIND>(hs);
+  return side_quarters<KIND>(hs) + side_mask_stores<KIND>(hs);
 }
 template <int KIND>
 __device__ __forceinline__ constexpr int side_vpg(int hs) {
@@ -267,14 +262,12 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
   // (the fragment reads' lgkmcnt waits are the compiler's, per MFMA)
   half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
                                                     [](auto) {});
-#ifndef NERF16_T_NOBARRIER
   // own DMA of chunk c+1 done: younger than it are chunk c+2's 4 pieces and, in the training
   // forward, at least this half-step's stores (all issued after chunk c+1's pieces)
   if constexpr (TAIL >= 1) {
     wait_vmcnt<TAIL >= 2 ? 4 + (SV ? side_stores<KIND>(HS0) : 0) : 0>();
     __builtin_amdgcn_s_barrier();
   }
-#endif
   // DMA of chunk c+3 into the slot chunk c-1 used, one piece after each tile's MFMAs: inside the
   // MFMA region (after the fragment reads, which the asm's memory clobber keeps ahead of it) the
   // pieces cost 1.2K cycles per layer; issued as a block between the half-steps, 2.4K
@@ -319,7 +312,16 @@ struct SaveAt {      // training forward: where a layer's activations go (see co
   uint32_t loff;                 // this lane's byte offset in them: ((lane & 31) * kSaveRow + 4h) * 4
   int hoff;                      // the layer's slice (floats), uniform
   bool valid;
+  __amdgpu_buffer_rsrc_t mrows;  // the wave's 32 ReLU-mask rows (layout.h kMaskRow)
+  uint32_t moff;                 // this lane's byte offset in them: (lane & 31) * kMaskRowBytes + 16h
+  int mlay;                      // the layer's mask slice: 32 * layer bytes, uniform
 };
+// The 16 mask bits of output tile T held by this lane (quarter q, element e -> bit 4q + e: neuron
+// 32T + 8q + 4h + e), at byte 2T of the lane's 16-byte word of the layer: exactly the 128-bit
+// mask the backward kernel folds from the activations (train.hip dgrad16), so it loads one word.
+__device__ __forceinline__ void mask_store(const SaveAt& sv, int T, uint32_t bits) {
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bits, sv.mrows, (int)sv.moff + 2 * T, sv.mlay, 0);
+}
 // 16 bytes at byte offset voff + 4 * (hoff + c) of the wave's rows: a buffer store, so the lane's
 // address stays one VGPR (the uniform slice goes in soffset, the constant in the offset field).
 __device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
@@ -335,9 +337,10 @@ __device__ __forceinline__ void load4(const float* bias, const float* ws, int h,
 // 32T + 8q + 4h + e of the layer's slice, the layout.h save order.
 template <int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const QuarterVec& qv, float s,
-                                         Operand (&in)[16], float& m, float& part, const SaveAt& sv) {
+                                         Operand (&in)[16], float& m, float& part, const SaveAt& sv, uint32_t& mb) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
   f32x4 rv;
+  uint32_t bits = 0u;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, qv.b[e]), 0.0f);
@@ -345,25 +348,21 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     m = fmaxf(m, r);
     if constexpr (SIGMA) part = fmaf(qv.w[e], r, part);
     split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
+    if constexpr (SV) bits |= (r > 0.0f ? 1u : 0u) << (4 * q + e);
   }
   if constexpr (SV) {
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
+    mb = q == 0 ? bits : (mb | bits);
+    if constexpr (q == 3) mask_store(sv, T, mb);
   }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
 template <int PH, int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const float* bias, const float* ws, int h,
                                         float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv,
-                                        const SaveAt& sv) {
-#ifdef NERF16_T_NOSIDE   // timing-only builds: no epilogue conversions (one register kept live); wrong results
-  if constexpr (PH == 1) {
-    constexpr int T = T0 + QG / 4, q = QG % 4;
-    asm volatile("" : "+v"(in[OP0 + QG / 2].hi) : "v"(acc[T][4 * q]));
-  }
-  return;
-#endif
+                                        const SaveAt& sv, uint32_t& mb) {
   if constexpr (PH == 0) load4<T0, QG, SIGMA>(bias, ws, h, qv);
-  else convert4<T0, OP0, QG, SIGMA, SV>(acc, inv, qv, s, in, m, part, sv);
+  else convert4<T0, OP0, QG, SIGMA, SV>(acc, inv, qv, s, in, m, part, sv, mb);
 }
 
 // PE operand Q split at scale s from this wave's LDS copy (layer 4 reads [h3, enc_x]): phase 0
@@ -398,7 +397,7 @@ __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
              const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
              float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
-             float* __restrict__ save, const float* __restrict__ encd) {
+             float* __restrict__ save, const float* __restrict__ encd, uint32_t* __restrict__ masks) {
   __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
   STAMP16(0);
@@ -414,6 +413,11 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
   // inside the MFMA schedule)
   const uint32_t loff = valid ? ((uint32_t)(lane & 31) * kSaveRow + 4 * h) * 4 : 0x40000000u;
+  __amdgpu_buffer_rsrc_t mrows;
+  if constexpr (SAVE)
+    mrows = __builtin_amdgcn_make_buffer_rsrc(masks + s0 * kMaskRow, (short)0, 32 * kMaskRowBytes, 0x00020000);
+  const uint32_t moff = valid ? (uint32_t)(lane & 31) * kMaskRowBytes + 16u * h : 0x40000000u;
+  uint32_t mb = 0u;   // training: ReLU-mask bits of the tile being converted
 
   // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
   float x[3];
@@ -500,7 +504,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // 4 quarters per half-step
   QuarterVec qv[4];
   float pe_v[8];
-  SaveAt sv_prev{wrows, loff, save_h(0), valid};   // training: save slices of y_{L-1}, y_L
+  SaveAt sv_prev{wrows, loff, save_h(0), valid, mrows, moff, 0};   // training: save slices of y_{L-1}, y_L
   SaveAt sv_cur = sv_prev;
   run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
                                        [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
@@ -508,7 +512,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
                                          static_for<4>([&](auto qc) __attribute__((always_inline)) {
                                            constexpr int j = decltype(qc)::value;
                                            quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false, SAVE>(
-                                               acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j], sv_cur);
+                                               acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j], sv_cur, mb);
                                          });
                                        });
   STAMP16(2);
@@ -539,10 +543,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs == 0) {
-      quarter<P, 4, 8, 0, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
-      quarter<P, 4, 8, 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1], sv_prev);
+      quarter<P, 4, 8, 0, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev, mb);
+      quarter<P, 4, 8, 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1], sv_prev, mb);
     } else if constexpr (hs <= 14) {
-      quarter<P, 4, 8, hs + 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
+      quarter<P, 4, 8, hs + 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev, mb);
     }
   };
   // group B's side: this layer's y_L tiles 0-3
@@ -550,10 +554,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
     constexpr bool sg = decltype(sigma_tag)::value;
     if constexpr (hs >= 1 && hs <= 14) {
-      quarter<P, 0, 0, hs - 1, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
+      quarter<P, 0, 0, hs - 1, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur, mb);
     } else if constexpr (hs == 15) {
-      quarter<P, 0, 0, 14, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
-      quarter<P, 0, 0, 15, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1], sv_cur);
+      quarter<P, 0, 0, 14, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur, mb);
+      quarter<P, 0, 0, 15, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1], sv_cur, mb);
     }
   };
   using NoSigma = std::false_type;
@@ -566,6 +570,8 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     if constexpr (SAVE) {
       sv_prev.hoff = save_h(L - 1);
       sv_cur.hoff = save_h(L);
+      sv_prev.mlay = kMaskLayerBytes * (L - 1);
+      sv_cur.mlay = kMaskLayerBytes * L;
     }
     // group A (k-steps 0..15, + PE 16..19 at layer 4)
     if (L == kSkipLayer) {
@@ -628,7 +634,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
         : "memory");
   }
   inv_cur = cst[kS16InvW + 8] / s_cur;
-  if constexpr (SAVE) sv_prev.hoff = save_h(7);
+  if constexpr (SAVE) {
+    sv_prev.hoff = save_h(7);
+    sv_prev.mlay = kMaskLayerBytes * 7;
+  }
   run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
   STAMP16(10);
@@ -653,9 +662,16 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
           hd[e] = rd[e] + ap[e];
         }
         if constexpr (SAVE) {
-          const SaveAt at{wrows, loff, 0, true};
+          const SaveAt at{wrows, loff, 0, true, mrows, moff, 0};
           save_store(at, kSaveRDir + t * 32 + 8 * q, rd);
           save_store(at, kSaveHd + t * 32 + 8 * q, hd);
+          uint32_t bits = 0u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bits |= (rd[e] > 0.0f ? 1u : 0u) << (4 * q + e);
+          mb = q == 0 ? bits : (mb | bits);
+          if (q == 3)   // r_dir's 64 bits per lane after the 8 layers: byte 256 + 8h + 2t
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)mb, mrows, (int)(moff - 8u * h) + 2 * t,
+                                                  kMaskRDirByte, 0);
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -702,17 +718,18 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
-                 float* save, const float* encd) {
+                 float* save, const float* encd, uint32_t* masks) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   constexpr int per_block = 32 * kW16Waves;
   const int64_t blocks = (M + per_block - 1) / per_block;
+  if (save && !masks) return set_error(NERF_ERR_BAD_ARG, "mlp16 training forward: mask rows required");
   if (save)
     hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, save, encd);
+                       feat, rgb, sigma, out_slot, out_T, save, encd, masks);
   else
     hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr);
+                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr, nullptr);
   return check_launch("mlp16_kernel");
 }
 

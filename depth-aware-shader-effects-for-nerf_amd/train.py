@@ -182,7 +182,8 @@ class Trainer:
         dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
         feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save, grad = torch.empty(M, 2400, device=dev), torch.empty(M, 2312, device=dev)
+        save, grad = torch.empty(M, _lib.SAVE_ROW, device=dev), torch.empty(M, _lib.GRAD_ROW, device=dev)
+        masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev)
         rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
         dsig, drgb, sq = torch.empty(M, device=dev), torch.empty(M, 3, device=dev), torch.empty(B, device=dev)
         grads = [torch.empty_like(self.view(self.grad, i)) for i in range(24)]
@@ -205,14 +206,15 @@ class Trainer:
         ck(lib.nerf_ray_features_train(P(self.packed), P(dn), B, P(app), rows, P(feat), P(encd), s), "features")
         ev[2].record(cur)
         ck(lib.nerf_mlp_forward_train(P(self.packed), P(o), P(dn), P(z), B, N, P(feat), P(encd), P(rgb), P(sigma),
-                                      P(save), s), "mlp_forward_train")
+                                      P(save), P(masks), s), "mlp_forward_train")
         ev[3].record(cur)
         ck(lib.nerf_composite(P(rgb), P(sigma), P(z), B, N, P(rgb_map), P(depth), None, s), "composite")
         ck(lib.nerf_composite_backward(P(rgb), P(sigma), P(z), P(rgb_map), P(tgt), B, N, 2.0 / (3 * B), P(dsig),
                                        P(drgb), P(sq), s), "composite_backward")
         ev[4].record(cur)
-        ck(lib.nerf_mlp_backward(P(self.packed), P(self.packedT), P(save), P(sigma), P(rgb), P(dsig), P(drgb), M,
-                                 P(grad), s), "mlp_backward")
+        mk = masks if _lib.get_mlp_arith() == "f16x3" else None
+        ck(lib.nerf_mlp_backward(P(self.packed), P(self.packedT), P(save), P(mk), P(sigma), P(rgb), P(dsig), P(drgb),
+                                 M, P(grad), s), "mlp_backward")
         ev[5].record(cur)
         ck(lib.nerf_param_grads(P(save), P(grad), M, N, P(app), rows, P(self.packed), gptr, P(self.dapp), P(ws),
                                 wsz, s), "param_grads")

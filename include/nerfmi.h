@@ -42,7 +42,8 @@ enum nerf_status {
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* nerf_last_error(void);
-/* ABI version (bumped on any signature or layout change; 6: nerf_effect_toon takes double levels). */
+/* ABI version (bumped on any signature or layout change; 7: ReLU mask rows in the training forward
+ * and backward, include/nerfmi_train.h). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays

@@ -28,6 +28,9 @@ extern "C" {
 /* Per-sample rows the forward saves / the backward writes (floats). */
 #define NERF_SAVE_ROW 2400 /* [h0..h3 | enc_x(64) | h4..h7 | enc_d(32) | r_dir(128) | hd(128)] */
 #define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dhd(128) | drgb(3)+pad | dsigma+pad] */
+/* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):
+ * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes. */
+#define NERF_MASK_ROW 68
 
 /* ---------------------------------------------------------------- whole step
  * Forward of train.py:77-84 (coarse volume_render, n_importance ignored as in
@@ -56,21 +59,25 @@ int nerf_pack_weights_transposed_host(const float* const* params, float* packedT
 /* nerf_ray_features plus enc_d (R,32): PE_4(d) (models.py:122), zero-padded. */
 int nerf_ray_features_train(const float* packed, const float* dirs, int64_t R, const float* app,
                             int64_t app_rows, float* feat, float* enc_d, nerf_stream_t stream);
-/* nerf_mlp_forward (no scatter) that also writes save (R*N, NERF_SAVE_ROW). */
+/* nerf_mlp_forward (no scatter) that also writes save (R*N, NERF_SAVE_ROW) and, under the f16x3
+ * arithmetic, masks (R*N, NERF_MASK_ROW) (required there; ignored under f32, may be null). */
 int nerf_mlp_forward_train(const float* packed, const float* origins, const float* dirs,
                            const float* z_vals, int64_t R, int N, const float* ray_feat,
                            const float* enc_d, float* rgb, float* sigma, float* save,
-                           nerf_stream_t stream);
+                           uint32_t* masks, nerf_stream_t stream);
 /* d/d(sigma, rgb) of the composite (render.py:66-78) given g = scale*(rgb_map - target);
  * sq_err (B) = per-ray sum of squared errors. */
 int nerf_composite_backward(const float* rgb, const float* sigma, const float* z_vals,
                             const float* rgb_map, const float* target, int64_t B, int N,
                             float scale, float* dsigma, float* drgb, float* sq_err,
                             nerf_stream_t stream);
-/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW). */
+/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW).  The ReLU
+ * masks come from `masks` when non-null (the f16x3 forward's; same arithmetic on both sides), else
+ * from the saved activations. */
 int nerf_mlp_backward(const float* packed, const float* packedT, const float* save,
-                      const float* sigma, const float* rgb, const float* dsigma, const float* drgb,
-                      int64_t M, float* grad, nerf_stream_t stream);
+                      const uint32_t* masks, const float* sigma, const float* rgb,
+                      const float* dsigma, const float* drgb, int64_t M, float* grad,
+                      nerf_stream_t stream);
 /* Every parameter gradient (+ appearance rows) from save and grad rows. */
 size_t nerf_param_grads_workspace_bytes(int64_t M);
 int nerf_param_grads(const float* save, const float* grad, int64_t M, int N, const float* app,

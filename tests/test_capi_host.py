@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -55,7 +55,7 @@ def test_bad_arguments_are_reported_not_launched():
     ws = lib.nerf_wgrad_workspace_bytes(5000, 256, 256)
     assert ws == 3 * 256 * 257 * 4                      # 2048-sample chunks x N x (K + bias column)
     assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2312) * 4
-    assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, 0, None, None) == 0
+    assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, None, 0, None, None) == 0
     # post effects
     assert lib.nerf_effect_workspace_bytes(0, 8) == 0
     assert lib.nerf_effect_workspace_bytes(800, 800) >= 256 + 2 * 800 * 800 * 4
