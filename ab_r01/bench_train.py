@@ -1,0 +1,206 @@
+"""Benchmark of the training step (BASELINE config 5).
+
+    python bench_train.py [--gpus N] [--steps K] [--warmup W] [--batch 4096]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench_train.py --gpus N
+
+One step = one iteration of the reference's train_nerf (src/train.py:77-92) per GPU on a
+4096-ray batch of one image, 64 stratified samples per ray (perturb=True; n_importance is
+ignored by the reference's volume_render, render.py:83-86): weight packing, forward with
+activation saves, mse loss, backward (composite, MLP data gradients, weight gradients), the
+data-parallel RCCL all-reduce of the flat gradient buffer, and the Adam update.  Batches come
+from the teacher-rendered synthetic scene (nerfmi.dataset.SyntheticNeRFDataset at 800x800; no
+dataset exists here) and are generated before the timed region (inputs resident in HBM).
+Rank 0 prints one JSON line; value = rays trained per second over all ranks (weak scaling:
+4096 rays per GPU per step).
+
+roofline: per-sample algorithmic FLOP of the three MFMA kernels (forward 1,048,832; data
+gradients 983,040; weight gradients 1,066,752 including bias columns — DESIGN.md §Training)
+over their event-timed durations.  The forward runs on the MLP arithmetic selected by --arith
+(f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
+157.3).  Under f16x3 the data gradients run on split-f16 MFMA too (838.9) and the weight
+gradients on bf16x6 MFMA (six bf16 products per fp32 product: 2516.8/6 = 419.5 TFLOP/s); under
+f32 both run on fp32 MFMA (157.3).
+cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on a 1024-ray
+batch on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+MFMA_F32_PEAK_TFLOPS = 157.3
+FLOP_FWD = 1_048_832
+FLOP_DGRAD = 2 * (7 * 256 * 256 + 256 * 128)                                   # 983,040
+FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 128 + 129 * 3)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="forward MLP MFMA arithmetic")
+    return p.parse_args()
+
+
+def cpu_baseline(target_s):
+    from oracle import nerf_oracle as O
+    from nerfmi import cameras
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    state = O.random_state(0)
+    torch.manual_seed(1)
+    table = torch.randn(100, 32)
+    o, d = O.get_rays(800, 800, cameras.synthetic_focal(800), cameras.frame_c2w("chair"))
+    o, d = o.reshape(-1, 3), d.reshape(-1, 3)
+    g = torch.Generator().manual_seed(3)
+    B = 1024
+    opt, n, t = None, 0, 0.0
+    while t < target_s and n < 50:
+        sel = torch.randperm(o.shape[0], generator=g)[:B]
+        t_rand = torch.rand(B, 64, generator=g)
+        target = torch.rand(B, 3, generator=g)
+        t0 = time.perf_counter()
+        _, _, _, opt = O.train_step(state, table, 0, o[sel], d[sel], target, 2.0, 6.0, 64, t_rand, optimizer=opt)
+        t += time.perf_counter() - t0
+        n += 1
+    return {"value": n * B / t, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} training steps of {B} rays (64 samples, fwd+bwd+Adam), oracle/nerf_oracle.py "
+                      f"train_step on PyTorch-CPU fp32, {t:.1f} s"}
+
+
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary_train.json")
+WGRAD_LAUNCHES = 12   # train.hip param_grads: 11 layer jobs + the appearance projection, each GEMM + reduction
+
+
+def pmc_traffic():
+    """HBM bytes per step of the weight-gradient phase and per data-gradient launch, from the
+    committed PMC passes of `scripts/profile_pmc.sh <dir> train` (2 x FETCH_SIZE + WRITE_SIZE)."""
+    try:
+        k = json.load(open(PMC_SUMMARY))["kernels"]
+        wgrad = WGRAD_LAUNCHES * (k["nerf::wgrad_bf_kernel"]["hbm_bytes_per_dispatch"]
+                                  + k["nerf::wgrad_reduce_kernel"]["hbm_bytes_per_dispatch"])
+        return {"wgrad": wgrad, "mlp_backward": k["nerf::mlp_backward16_kernel"]["hbm_bytes_per_dispatch"]}
+    except (OSError, KeyError, ValueError):
+        return {}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    import nerfmi
+    from nerfmi import _lib
+    from nerfmi.dataset import SyntheticNeRFDataset
+    from nerfmi.train import Trainer
+    nerfmi.set_mlp_arith(args.arith)
+    cfg = nerfmi.Config()
+    np.random.seed(100 + rank)                    # each rank draws its own images / pixels
+    ds = SyntheticNeRFDataset(cfg, n_images=100)
+    batches = [ds.get_rays(batch_size=args.batch) for _ in range(args.warmup + args.steps)]
+    torch.manual_seed(0)
+    tr = Trainer(cfg, appearance_embeddings=ds.appearance_embeddings, group=group)
+    lib, P = _lib.load(), _lib.ptr
+    stream = torch.cuda.current_stream()
+
+    # stage timing: events around each stage on the launch stream
+    ev = {k: [] for k in ("fwd", "bwd", "allreduce", "adam")}
+
+    def step(b, timed):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
+        if timed:
+            marks[0].record(stream)
+        tr.forward_backward(b["rays_o"], b["rays_d"], b["rgb"], b["appearance_idx"], seed=tr.steps + 1,
+                            _marks=marks)
+        if timed:
+            marks[2].record(stream)
+        tr.all_reduce()
+        if timed:
+            marks[3].record(stream)
+        tr.optimizer_step()
+        if timed:
+            marks[4].record(stream)
+            ev["_pending"] = ev.get("_pending", []) + [marks]
+
+    for i in range(args.warmup):
+        step(batches[i], False)
+    if group is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(batches[args.warmup + i], True)
+    torch.cuda.synchronize()
+    if group is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if group is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    stage = {"fwd": [], "bwd": [], "allreduce": [], "adam": []}
+    for m in ev.get("_pending", []):
+        stage["fwd"].append(m[0].elapsed_time(m[1]))
+        stage["bwd"].append(m[1].elapsed_time(m[2]))
+        stage["allreduce"].append(m[2].elapsed_time(m[3]))
+        stage["adam"].append(m[3].elapsed_time(m[4]))
+    stage_ms = {k: float(np.mean(v)) for k, v in stage.items()}
+    # kernel-level timing of one extra (untimed) step: forward, data-gradient and weight-gradient phases
+    kt = tr.profile_step(batches[-1]["rays_o"], batches[-1]["rays_d"], batches[-1]["rgb"],
+                         batches[-1]["appearance_idx"])
+    if rank == 0:
+        M = args.batch * cfg.num_samples
+        rays = args.batch * args.steps * world
+        kern = {"mlp_forward_train": (FLOP_FWD, kt["mlp_forward_ms"]), "mlp_backward": (FLOP_DGRAD, kt["mlp_backward_ms"]),
+                "wgrad": (FLOP_WGRAD, kt["param_grads_ms"])}
+        peaks = {"mlp_forward_train": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
+                 "mlp_backward": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
+                 "wgrad": MFMA_F32_PEAK_TFLOPS * (16 / 6 if args.arith == "f16x3" else 1)}
+        dominant = max(kern, key=lambda k: kern[k][1])
+        flop, ms = kern[dominant]
+        ach = M * flop / (ms * 1e-3) / 1e12
+        traffic = pmc_traffic() if args.arith == "f16x3" else {}
+        out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
+               "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic: teacher-rendered 800x800 scene (SyntheticNeRFDataset, 100 poses), batches "
+                       "pre-generated in HBM; student = torch.manual_seed(0); NeRF(Config())",
+               "config": {"workload": "chair-style training loop, one image per batch", "rays_per_gpu_per_step":
+                          args.batch, "n_samples": cfg.num_samples, "parallelism": f"dp{world} (RCCL all-reduce)"},
+               "mlp_arith_forward": args.arith,
+               "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": peaks[dominant],
+                            "unit": "TFLOP/s", "frac": ach / peaks[dominant],
+                            "traffic": traffic.get(dominant), "traffic_unit": "bytes/phase (one step)",
+                            "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
+                            if traffic.get(dominant) is not None else None,
+                            "traffic_by_kernel": traffic,
+                            "kernels_ms": {k: v[1] for k, v in kern.items()},
+                            "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()},
+                            "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()}},
+               "stage_ms": stage_ms, "phase_ms": kt}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if group is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,73 @@
+// Internal helpers shared by the HIP translation units of libnerfmi.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <utility>
+#include "../../include/nerfmi_train.h"
+#include "layout.h"
+
+namespace nerf {
+
+// Records the message of a failed call for nerf_last_error() and returns `code`.
+int set_error(int code, const char* fmt, ...);
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NERF_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return NERF_OK;
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, fully expanded by the
+// front end (the loop unroller gives up on bodies this large and would leave the register
+// arrays runtime-indexed, i.e. in scratch).
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+// Counter-based uniform in [0,1) (splitmix64 finaliser), used when the caller
+// passes no explicit uniforms; it is a device RNG for throughput runs only.
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// Kernel launchers (one per translation unit); each returns a nerf_status.
+int launch_get_rays(int H, int W, float focal, const float* c2w, int row0, int nrows,
+                    float* o, float* d, hipStream_t s);
+int launch_pe(const float* x, int64_t M, int dims, int levels, int include_input, float* out, hipStream_t s);
+int launch_normalize(const float* d, int64_t B, float* out, hipStream_t s);
+int launch_stratified(const float* o, const float* d, int64_t B, float near_f, float span_f,
+                      int N, const float* t_vals, int perturb, const float* t_rand,
+                      uint64_t seed, float* z, float* pts, hipStream_t s);
+int launch_importance(const float* o, const float* d, const float* z, const float* w,
+                      int64_t B, int N, int Nf, const float* u_lin, const float* u_rand,
+                      uint64_t seed, float* z_all, float* pts_all, const float* rgb_c, const float* sigma_c,
+                      float* rgb_all, float* sigma_all, float* z_fine, int* fine_slot, hipStream_t s);
+int launch_pack(const float* const* params, float* packed, hipStream_t s);
+int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
+                        int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
+extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
+int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
+                 const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
+                 float* save = nullptr, const float* encd = nullptr);
+int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
+               int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
+               hipStream_t s, float* save = nullptr, const float* encd = nullptr);
+int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N,
+                     float* rgb_map, float* depth, float* weights, hipStream_t s);
+
+}  // namespace nerf

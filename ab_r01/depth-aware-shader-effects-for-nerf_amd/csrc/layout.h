@@ -183,16 +183,6 @@ constexpr int kSaveEncD = 1088 + 4 * kHidden;                // 2112
 constexpr int kSaveRDir = kSaveEncD + 32;                    // 2144
 constexpr int kSaveHd = kSaveRDir + kDirHidden;              // 2272
 constexpr int kSaveRow = kSaveHd + kDirHidden;               // 2400 floats per sample
-// Training ReLU masks (written by the f16x3 forward, read by the split-f16 backward), one row of
-// 272 bytes per sample in their own buffer: for trunk layer l, 32 bytes = lane half h's 16-byte
-// slot at 32 l + 16 h (tile T's 16 bits at byte 2T, bit 4q + e = neuron 32T + 8q + 4h + e), then
-// r_dir's 8 bytes per lane half at 256 + 8h.  The backward reads one slot per layer instead of the
-// layer's 1 KiB of f32 activations.  (Kept out of the save rows: a 2,496-float row stride cost the
-// training forward 9 %, same-box A/B.)
-constexpr int kMaskLayerBytes = 32;
-constexpr int kMaskRDirByte = 8 * kMaskLayerBytes;           // 256
-constexpr int kMaskRowBytes = kMaskRDirByte + 16;            // 272
-constexpr int kMaskRow = kMaskRowBytes / 4;                  // 68 words per sample
 
 // Per-sample gradient row written by the backward pass (nerf_mlp_backward):
 //   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dhd (128) | drgb_pre (3) + pad | dsigma_pre + pad]

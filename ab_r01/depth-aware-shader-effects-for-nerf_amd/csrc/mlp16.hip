@@ -91,11 +91,6 @@ constexpr int kLdsRgb = kLdsConsts + kS16Consts;             // rgb_linear weigh
 constexpr int kLdsRgbFloats = 3 * kDirHidden + 4;
 constexpr int kLdsFeat = kLdsRgb + kLdsRgbFloats;             // per wave: its ray's features (256)
 constexpr int kLdsFloats = kLdsFeat + kW16Waves * kRayFeat;   // 111 KiB
-// Training forward only: each wave's 32 ReLU-mask rows (layout.h kMaskRow words, 272 B per
-// sample), accumulated by ds_or from the epilogue quarters and copied out at the end.
-constexpr int kMaskWords = kMaskRow;                          // 68
-constexpr int kLdsMask = kLdsFloats;
-constexpr int kLdsFloatsSave = kLdsMask + kW16Waves * 32 * kMaskWords;   // 145 KiB
 static_assert(kOffRgbB == kOffRgbW + 3 * kDirHidden && kLdsRgb % 4 == 0 && kLdsFeat % 4 == 0, "LDS vector layout");
 static_assert(kOffSigmaW == kOffBias + 8 * kHidden && kOffSigmaB == kOffSigmaW + kHidden, "packed vector order");
 
@@ -117,6 +112,9 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
                                                 uint32_t voff) {
+#ifdef NERF16_T_NODMA
+  return;
+#endif
   const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
 #ifdef NERF16_M0_SAVE
   uint32_t keep;
@@ -157,6 +155,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 // A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
 template <int KK>
 __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
+#ifdef NERF16_T_NOREAD
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
+  return;
+#endif
 #pragma unroll
   for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
@@ -168,6 +171,11 @@ __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], 
 // One k-step of group G (tiles 4G .. 4G+3).
 template <int G, bool FIRST, typename Hook>
 __device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8], Hook&& hook) {
+#ifdef NERF16_T_NOMFMA   // timing-only builds (scripts/microbench/mlp16_stamps.hip); wrong results
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[4 * G + i]) : "v"(a[i][0]), "v"(a[i][1]), "v"(b.hi), "v"(b.lo));
+  return;
+#endif
   static_for<4>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     f32x16 c;
@@ -259,12 +267,14 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
   // (the fragment reads' lgkmcnt waits are the compiler's, per MFMA)
   half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
                                                     [](auto) {});
+#ifndef NERF16_T_NOBARRIER
   // own DMA of chunk c+1 done: younger than it are chunk c+2's 4 pieces and, in the training
   // forward, at least this half-step's stores (all issued after chunk c+1's pieces)
   if constexpr (TAIL >= 1) {
     wait_vmcnt<TAIL >= 2 ? 4 + (SV ? side_stores<KIND>(HS0) : 0) : 0>();
     __builtin_amdgcn_s_barrier();
   }
+#endif
   // DMA of chunk c+3 into the slot chunk c-1 used, one piece after each tile's MFMAs: inside the
   // MFMA region (after the fragment reads, which the asm's memory clobber keeps ahead of it) the
   // pieces cost 1.2K cycles per layer; issued as a block between the half-steps, 2.4K
@@ -309,16 +319,7 @@ struct SaveAt {      // training forward: where a layer's activations go (see co
   uint32_t loff;                 // this lane's byte offset in them: ((lane & 31) * kSaveRow + 4h) * 4
   int hoff;                      // the layer's slice (floats), uniform
   bool valid;
-  unsigned* mrow;                // this lane's mask words in LDS: the sample's row + 4h (words)
-  int mlay;                      // the layer's words in the row: 8 * layer, uniform
 };
-// ReLU-mask bits of tile T (quarter q, element e -> bit 4q + e: neuron 32T + 8q + 4h + e) go to
-// bits 16 (T % 2) of word T / 2 of the lane's 4-word (16-byte) slot of the layer: exactly the
-// 128-bit mask the backward folds from the activations (train.hip dgrad16), so it loads one slot.
-// One ds_or per quarter: no register lives across quarters.
-__device__ __forceinline__ void mask_or(const SaveAt& sv, int T, uint32_t bits) {
-  __hip_atomic_fetch_or(sv.mrow + sv.mlay + T / 2, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
 // 16 bytes at byte offset voff + 4 * (hoff + c) of the wave's rows: a buffer store, so the lane's
 // address stays one VGPR (the uniform slice goes in soffset, the constant in the offset field).
 __device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
@@ -336,9 +337,7 @@ template <int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, const QuarterVec& qv, float s,
                                          Operand (&in)[16], float& m, float& part, const SaveAt& sv) {
   constexpr int T = T0 + QG / 4, q = QG % 4;
-  constexpr int SH = 16 * (T % 2) + 4 * q;
   f32x4 rv;
-  uint32_t bits = 0u;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float r = fmaxf(fmaf(acc[T][4 * q + e], inv, qv.b[e]), 0.0f);
@@ -346,11 +345,9 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     m = fmaxf(m, r);
     if constexpr (SIGMA) part = fmaf(qv.w[e], r, part);
     split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
-    if constexpr (SV) bits |= (r > 0.0f ? 1u : 0u) << (SH + e);
   }
   if constexpr (SV) {
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
-    mask_or(sv, T, bits);
   }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
@@ -358,6 +355,13 @@ template <int PH, int T0, int OP0, int QG, bool SIGMA, bool SV>
 __device__ __forceinline__ void quarter(const f32x16 (&acc)[8], float inv, const float* bias, const float* ws, int h,
                                         float s, Operand (&in)[16], float& m, float& part, QuarterVec& qv,
                                         const SaveAt& sv) {
+#ifdef NERF16_T_NOSIDE   // timing-only builds: no epilogue conversions (one register kept live); wrong results
+  if constexpr (PH == 1) {
+    constexpr int T = T0 + QG / 4, q = QG % 4;
+    asm volatile("" : "+v"(in[OP0 + QG / 2].hi) : "v"(acc[T][4 * q]));
+  }
+  return;
+#endif
   if constexpr (PH == 0) load4<T0, QG, SIGMA>(bias, ws, h, qv);
   else convert4<T0, OP0, QG, SIGMA, SV>(acc, inv, qv, s, in, m, part, sv);
 }
@@ -394,8 +398,8 @@ __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
              const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
              float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
-             float* __restrict__ save, const float* __restrict__ encd, uint32_t* __restrict__ masks) {
-  __shared__ __attribute__((aligned(16))) float lds[SAVE ? kLdsFloatsSave : kLdsFloats];
+             float* __restrict__ save, const float* __restrict__ encd) {
+  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
   STAMP16(0);
   const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
@@ -410,12 +414,6 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
   // inside the MFMA schedule)
   const uint32_t loff = valid ? ((uint32_t)(lane & 31) * kSaveRow + 4 * h) * 4 : 0x40000000u;
-  // training: this wave's mask rows in LDS, zeroed before the quarters OR their bits in
-  unsigned* mwave = reinterpret_cast<unsigned*>(lds + kLdsMask) + wave * 32 * kMaskWords;
-  unsigned* mrow = mwave + (lane & 31) * kMaskWords + 4 * h;
-  if constexpr (SAVE) {
-    for (int i = lane; i < 32 * kMaskWords; i += 64) mwave[i] = 0u;
-  }
 
   // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
   float x[3];
@@ -502,7 +500,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   // 4 quarters per half-step
   QuarterVec qv[4];
   float pe_v[8];
-  SaveAt sv_prev{wrows, loff, save_h(0), valid, mrow, 0};   // training: save slices of y_{L-1}, y_L
+  SaveAt sv_prev{wrows, loff, save_h(0), valid};   // training: save slices of y_{L-1}, y_L
   SaveAt sv_cur = sv_prev;
   run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
                                        [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
@@ -568,8 +566,6 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     if constexpr (SAVE) {
       sv_prev.hoff = save_h(L - 1);
       sv_cur.hoff = save_h(L);
-      sv_prev.mlay = (kMaskLayerBytes / 4) * (L - 1);
-      sv_cur.mlay = (kMaskLayerBytes / 4) * L;
     }
     // group A (k-steps 0..15, + PE 16..19 at layer 4)
     if (L == kSkipLayer) {
@@ -632,10 +628,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
         : "memory");
   }
   inv_cur = cst[kS16InvW + 8] / s_cur;
-  if constexpr (SAVE) {
-    sv_prev.hoff = save_h(7);
-    sv_prev.mlay = (kMaskLayerBytes / 4) * 7;
-  }
+  if constexpr (SAVE) sv_prev.hoff = save_h(7);
   run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
   STAMP16(10);
@@ -660,15 +653,9 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
           hd[e] = rd[e] + ap[e];
         }
         if constexpr (SAVE) {
-          const SaveAt at{wrows, loff, 0, true, mrow, 0};
+          const SaveAt at{wrows, loff, 0, true};
           save_store(at, kSaveRDir + t * 32 + 8 * q, rd);
           save_store(at, kSaveHd + t * 32 + 8 * q, hd);
-          uint32_t bits = 0u;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bits |= (rd[e] > 0.0f ? 1u : 0u) << (16 * (t % 2) + 4 * q + e);
-          // r_dir: 8 bytes per lane half at byte 256 + 8h of the row (mrow holds + 4h words)
-          __hip_atomic_fetch_or(mrow - 2 * h + kMaskRDirByte / 4 + t / 2, bits, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -684,18 +671,11 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   } else {
     colour_head(feat + r * kRayFeat);
   }
-  if constexpr (SAVE) {   // the wave's 32 mask rows: 8,704 contiguous bytes in LDS and in `masks`
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int n16 = (int)imin64(M - s0, 32) * (kMaskWords / 4);
-    u32x4v* dst = reinterpret_cast<u32x4v*>(masks + s0 * kMaskWords);
-    for (int i = lane; i < n16; i += 64) dst[i] = reinterpret_cast<const u32x4v*>(mwave)[i];
-  }
   float out[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
-    out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
+    out[c] = 1.0f / (1.0f + expf(-v));                           // sigmoid (models.py:159-160)
   }
   if constexpr (SAVE) {
     if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d
@@ -722,18 +702,17 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
-                 float* save, const float* encd, uint32_t* masks) {
+                 float* save, const float* encd) {
   const int64_t M = R * (int64_t)N;
   if (M == 0) return NERF_OK;
   constexpr int per_block = 32 * kW16Waves;
   const int64_t blocks = (M + per_block - 1) / per_block;
-  if (save && !masks) return set_error(NERF_ERR_BAD_ARG, "mlp16 training forward: mask rows required");
   if (save)
     hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, save, encd, masks);
+                       feat, rgb, sigma, out_slot, out_T, save, encd);
   else
     hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr, nullptr);
+                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr);
   return check_launch("mlp16_kernel");
 }
 

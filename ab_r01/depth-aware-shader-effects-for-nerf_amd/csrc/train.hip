@@ -65,7 +65,7 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
     if (s < N) {
       const float z = zv[base + s];
       const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
-      const float alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
+      const float alpha = 1.0f - expf(-sigma[base + s] * dist);
       f = (double)((1.0f - alpha) + 1e-10f);
     }
     double incl = f;
@@ -88,7 +88,7 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
       const float z = zv[base + s];
       dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
       sg = sigma[base + s];
-      e = expf_rn(-sg * dist);
+      e = expf(-sg * dist);
       alpha = 1.0f - e;
       fs = (1.0f - alpha) + 1e-10f;
       f = (double)fs;
@@ -357,7 +357,11 @@ __device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, cons
     if (t >= ntiles) break;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+#ifdef NERF_BW16_ABL_SAVE      // timing only: no activation loads
+      const f32x4 a = {x[t][4 * q], x[t][4 * q + 1], x[t][4 * q + 2], x[t][4 * q + 3]};
+#else
       const f32x4 a = *reinterpret_cast<const f32x4*>(srow + save_off + t * 32 + 8 * q + 4 * h);
+#endif
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -496,20 +500,15 @@ __device__ __forceinline__ void fold_mask(uint32_t (&mask)[4], int c, f32x4 a) {
   for (int e = 0; e < 4; ++e) mask[c / 8] |= (a[e] > 0.0f ? 1u : 0u) << (4 * (c % 8) + e);
 }
 
-// MB: the mask is the forward's 128-bit word for this lane (`mword`, one 16-byte load issued
-// first and waited for only after the MFMA chain), and `act` is unused.
-template <int KS, bool MB>
+template <int KS>
 __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const h16x8 (&bh)[16],
                                         const h16x8 (&bl)[16], f32x16 (&out)[8], float inv_w, float inv_g,
-                                        const float* __restrict__ act, const uint32_t* __restrict__ mword,
-                                        uint32_t (&mask)[4], int lane) {
+                                        const float* __restrict__ act, uint32_t (&mask)[4], int lane) {
   constexpr int STEPS = 2 * KS, PIECES = 8 * STEPS, DEPTH = 24;
   constexpr int CPS = 32 / STEPS, LAG = 3, RS = (LAG + 1) * CPS;   // mask chunks per step, load->fold lag
   const u32x4* __restrict__ wf = reinterpret_cast<const u32x4*>(wmat) + lane;
   u32x4 ring[DEPTH];
   f32x4 pf[RS];
-  u32x4 mk;
-  if constexpr (MB) mk = *reinterpret_cast<const u32x4*>(mword);
 #pragma unroll
   for (int i = 0; i < 4; ++i) mask[i] = 0u;
 #pragma unroll
@@ -517,16 +516,14 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
   sfor<STEPS>([&](auto sc) __attribute__((always_inline)) {
     constexpr int st = decltype(sc)::value;
     constexpr int g = st / KS, ks = st % KS;
-    if constexpr (!MB && st >= LAG) {
+    if constexpr (st >= LAG) {
 #pragma unroll
       for (int u = 0; u < CPS; ++u) fold_mask(mask, (st - LAG) * CPS + u, pf[((st - LAG) * CPS + u) % RS]);
     }
-    if constexpr (!MB) {
 #pragma unroll
-      for (int u = 0; u < CPS; ++u) {
-        const int c = st * CPS + u;
-        pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
-      }
+    for (int u = 0; u < CPS; ++u) {
+      const int c = st * CPS + u;
+      pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
     }
     if constexpr (ks == 0) {
 #pragma unroll
@@ -547,7 +544,11 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
     });
     sfor<8>([&](auto qc) __attribute__((always_inline)) {
       constexpr int p = 8 * st + decltype(qc)::value;
+#ifdef NERF_BW16_ABL_WEIGHTS   // timing only: every step re-reads the first 24 pieces (L1-resident)
+      if constexpr (p + DEPTH < PIECES) ring[p % DEPTH] = wf[((p + DEPTH) % DEPTH) * 64];
+#else
       if constexpr (p + DEPTH < PIECES) ring[p % DEPTH] = wf[(p + DEPTH) * 64];
+#endif
     });
     if constexpr (ks == KS - 1) {
 #pragma unroll
@@ -555,21 +556,15 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
     }
     __builtin_amdgcn_sched_barrier(0);
   });
-  if constexpr (MB) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) mask[i] = mk[i];
-  } else {
-#pragma unroll
-    for (int c = (STEPS - LAG) * CPS; c < 32; ++c) fold_mask(mask, c, pf[c % RS]);
-  }
+  for (int c = (STEPS - LAG) * CPS; c < 32; ++c) fold_mask(mask, c, pf[c % RS]);
 }
 
-// relu_back_store with the mask from dgrad16 (tiles 0..NT-1)
-template <int NT = 8>
+// relu_back_store with the mask from dgrad16
 __device__ __forceinline__ void relu_mask_store(f32x16 (&x)[8], const uint32_t (&mask)[4], const GradRows& gr,
                                                 int grad_off) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < 8; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = 4 * t + q;
@@ -584,13 +579,9 @@ __device__ __forceinline__ void relu_mask_store(f32x16 (&x)[8], const uint32_t (
     }
 }
 
-// MB: ReLU masks from the f16x3 forward's mask rows (one 16-byte slot per layer and lane) instead
-// of the saved f32 activations (1 KiB per layer and sample).
-template <bool MB>
 __global__ void __launch_bounds__(256, 1)
 mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
-                      const float* __restrict__ save, const uint32_t* __restrict__ masks,
-                      const float* __restrict__ sigma, const float* __restrict__ rgb,
+                      const float* __restrict__ save, const float* __restrict__ sigma, const float* __restrict__ rgb,
                       const float* __restrict__ dsigma, const float* __restrict__ drgb, int64_t M,
                       float* __restrict__ grad) {
   const int lane = threadIdx.x & 63;
@@ -635,19 +626,10 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
       }
       grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
     }
-  const uint32_t* mrow = MB ? masks + s * kMaskRow : nullptr;
+  relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
   uint32_t mask[4];
-  if constexpr (MB) {
-    const uint32_t* md = mrow + (kMaskRDirByte + 8 * h) / 4;
-    mask[0] = md[0];
-    mask[1] = md[1];
-    relu_mask_store<4>(X, mask, gr, kGradDir);
-  } else {
-    relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
-  }
   float inv_g = split_rows<4>(X, bh, bl);
-  dgrad16<kDirHidden / 16, MB>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h,
-                               mrow + (kMaskLayerBytes * 7 + 16 * h) / 4, mask, lane);
+  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h, mask, lane);
   const float* wsg = packed + kOffSigmaW;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
@@ -661,23 +643,19 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   for (int l = 7; l >= 1; --l) {
     relu_mask_store(X, mask, gr, l * kHidden);
     inv_g = split_rows<8>(X, bh, bl);
-    dgrad16<kHidden / 16, MB>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h,
-                              mrow + (kMaskLayerBytes * (l - 1) + 16 * h) / 4, mask, lane);
+    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h,
+                          mask, lane);
   }
   relu_mask_store(X, mask, gr, 0);
 }
 
-int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
-                        const float* sigma, const float* rgb, const float* dsigma, const float* drgb, int64_t M,
-                        float* grad, hipStream_t s) {
+int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
+                        const float* rgb, const float* dsigma, const float* drgb, int64_t M, float* grad,
+                        hipStream_t s) {
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3) {
-    if (masks)
-      hipLaunchKernelGGL(mlp_backward16_kernel<true>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, save, masks, sigma, rgb, dsigma, drgb, M, grad);
-    else
-      hipLaunchKernelGGL(mlp_backward16_kernel<false>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, save, masks, sigma, rgb, dsigma, drgb, M, grad);
+    hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT,
+                       save, sigma, rgb, dsigma, drgb, M, grad);
     return check_launch("mlp_backward16_kernel");
   }
   hipLaunchKernelGGL(mlp_backward_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT, save,
@@ -1254,10 +1232,8 @@ __global__ void __launch_bounds__(256) loss_kernel(const float* __restrict__ sq_
 
 // Training workspace carve (each region 256-B aligned), M = B*N samples:
 //   dirs (B,3) | z (B,N) | feat (B,256) | encd (B,32) | rgb (M,3) | sigma (M) | maps (B,4)
-//   | dsigma (M) | drgb (M,3) | sq_err (B) | save (M,kSaveRow) | masks (M,kMaskRow) | grad (M,kGradRow)
-//   | wgrad partials
-enum { T_DIRS, T_Z, T_FEAT, T_ENCD, T_RGB, T_SIG, T_MAPS, T_DSIG, T_DRGB, T_SQE, T_SAVE, T_MASK, T_GRAD, T_WG,
-       T_COUNT };
+//   | dsigma (M) | drgb (M,3) | sq_err (B) | save (M,kSaveRow) | grad (M,kGradRow) | wgrad partials
+enum { T_DIRS, T_Z, T_FEAT, T_ENCD, T_RGB, T_SIG, T_MAPS, T_DSIG, T_DRGB, T_SQE, T_SAVE, T_GRAD, T_WG, T_COUNT };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1275,7 +1251,7 @@ static size_t max_wgrad_floats(int64_t M) {
 static size_t train_carve(int64_t B, int N, size_t* off) {
   const size_t b = (size_t)B, M = b * (size_t)N;
   const size_t sizes[T_COUNT] = {b * 3, b * N, b * kRayFeat, b * 32, M * 3, M, b * 4, M, M * 3, b,
-                                 M * kSaveRow, M * kMaskRow, M * kGradRow, max_wgrad_floats((int64_t)M)};
+                                 M * kSaveRow, M * kGradRow, max_wgrad_floats((int64_t)M)};
   size_t at = 0;
   for (int i = 0; i < T_COUNT; ++i) {
     off[i] = at;
@@ -1321,13 +1297,12 @@ int nerf_ray_features_train(const float* packed, const float* dirs, int64_t R, c
 
 int nerf_mlp_forward_train(const float* packed, const float* origins, const float* dirs, const float* z_vals,
                            int64_t R, int N, const float* ray_feat, const float* enc_d, float* rgb, float* sigma,
-                           float* save, uint32_t* masks, nerf_stream_t stream) {
+                           float* save, nerf_stream_t stream) {
   TREQUIRE(R >= 0 && N >= 1, "nerf_mlp_forward_train: R=%lld N=%d", (long long)R, N);
   TREQUIRE(R == 0 || (packed && origins && dirs && z_vals && ray_feat && enc_d && rgb && sigma && save),
            "nerf_mlp_forward_train: null pointer");
-  TREQUIRE(R == 0 || masks || g_mlp_arith != NERF_ARITH_F16X3, "nerf_mlp_forward_train: masks required under f16x3");
   return launch_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, nullptr, 0, (hipStream_t)stream, save,
-                    enc_d, masks);
+                    enc_d);
 }
 
 int nerf_composite_backward(const float* rgb, const float* sigma, const float* z_vals, const float* rgb_map,
@@ -1341,13 +1316,13 @@ int nerf_composite_backward(const float* rgb, const float* sigma, const float* z
                                    (hipStream_t)stream);
 }
 
-int nerf_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
-                      const float* sigma, const float* rgb, const float* dsigma, const float* drgb, int64_t M,
-                      float* grad, nerf_stream_t stream) {
+int nerf_mlp_backward(const float* packed, const float* packedT, const float* save, const float* sigma,
+                      const float* rgb, const float* dsigma, const float* drgb, int64_t M, float* grad,
+                      nerf_stream_t stream) {
   TREQUIRE(M >= 0, "nerf_mlp_backward: M=%lld", (long long)M);
   TREQUIRE(M == 0 || (packed && packedT && save && sigma && rgb && dsigma && drgb && grad),
            "nerf_mlp_backward: null pointer");
-  return launch_mlp_backward(packed, packedT, save, masks, sigma, rgb, dsigma, drgb, M, grad, (hipStream_t)stream);
+  return launch_mlp_backward(packed, packedT, save, sigma, rgb, dsigma, drgb, M, grad, (hipStream_t)stream);
 }
 
 size_t nerf_wgrad_workspace_bytes(int64_t M, int N, int K) {
@@ -1459,7 +1434,7 @@ int nerf_train_forward(const float* packed, const float* rays_o, const float* ra
     return rc;                                                                                          // :22
   if ((rc = launch_ray_features(packed, R(T_DIRS), B, app, app_rows, R(T_FEAT), s, R(T_ENCD)))) return rc;
   if ((rc = launch_mlp(packed, rays_o, R(T_DIRS), R(T_Z), B, N, R(T_FEAT), R(T_RGB), R(T_SIG), nullptr, 0, s,
-                       R(T_SAVE), R(T_ENCD), (uint32_t*)R(T_MASK))))
+                       R(T_SAVE), R(T_ENCD))))
     return rc;                                                                                          // :49
   return launch_composite(R(T_RGB), R(T_SIG), R(T_Z), B, N, rgb_map, depth_map, nullptr, s);           // :56-80
 }
@@ -1488,10 +1463,7 @@ int nerf_train_backward(const float* packed, const float* packedT, const float* 
     return rc;
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, R(T_SQE), B, loss);
   if ((rc = check_launch("loss_kernel"))) return rc;
-  // the f16x3 forward wrote the mask rows (nerf_train_forward under the same arithmetic)
-  const uint32_t* masks = g_mlp_arith == NERF_ARITH_F16X3 ? (const uint32_t*)R(T_MASK) : nullptr;
-  if ((rc = launch_mlp_backward(packed, packedT, R(T_SAVE), masks, R(T_SIG), R(T_RGB), R(T_DSIG), R(T_DRGB), M,
-                                R(T_GRAD), s)))
+  if ((rc = launch_mlp_backward(packed, packedT, R(T_SAVE), R(T_SIG), R(T_RGB), R(T_DSIG), R(T_DRGB), M, R(T_GRAD), s)))
     return rc;
   const size_t wg_floats = (need - off[T_WG]) / 4;
   return param_grads(R(T_SAVE), R(T_GRAD), M, N, app, app_rows, packed, param_grads_out, dapp, R(T_WG), wg_floats, s);

@@ -1,0 +1,101 @@
+"""Frame rendering sharded by ray chunk over the GPUs of one node.
+
+The reference renders a frame as a loop over independent ray chunks (run.py:209-231).
+Here the rays of a batch of frames — frame-major, row-major inside a frame, exactly the
+order run.py concatenates its chunks in (run.py:230-231) — are cut into one contiguous
+shard per rank.  Each rank generates only its own rays (get_rays on the rows it needs),
+renders them, and one all-gather (torch.distributed, backend "nccl" = RCCL over xGMI)
+reassembles [r, g, b, depth] of every ray on every rank in ray order.  Rays are independent
+and every ray costs the same, so there is no other exchange.
+
+With one pose and N ranks this is strong scaling of one frame; with N poses and N ranks
+each rank renders one whole frame (weak scaling, what bench.py measures).
+The ray source and the renderer are injectable so the sharding and reassembly logic is
+tested with gloo on CPU (tests/test_frames_dist.py) with no GPU.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_rays, world, rank):
+    """Contiguous [start, end) of rank `rank` and the padded shard length (all shards equal)."""
+    per = -(-n_rays // world) if n_rays else 0
+    start = min(rank * per, n_rays)
+    return start, min(start + per, n_rays), per
+
+
+def _world(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def shard_rays(ray_fn, H, W, n_frames, start, end):
+    """(o, d) of global rays [start, end): frame f = ray // (H*W), generated per frame on the
+    rows that hold the range and sliced to it.  ray_fn(frame, row0, nrows) -> (o, d), each
+    (nrows*W, 3)."""
+    P = H * W
+    os_, ds_ = [], []
+    r = start
+    while r < end:
+        f = r // P
+        lo = r - f * P
+        hi = min(end - f * P, P)
+        row0, row1 = lo // W, -(-hi // W)
+        o, d = ray_fn(f, row0, row1 - row0)
+        os_.append(o[lo - row0 * W: hi - row0 * W])
+        ds_.append(d[lo - row0 * W: hi - row0 * W])
+        r = f * P + hi
+    if not os_:
+        return None, None
+    return torch.cat(os_), torch.cat(ds_)
+
+
+def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=None):
+    """Render n_frames HxW frames over the ranks of `group`.
+
+    ray_fn(frame, row0, nrows) -> (rays_o, rays_d) for those rows (row-major, (nrows*W, 3));
+    render_fn(rays_o, rays_d, ray_offset) -> (rgb (n,3), depth (n,1)); ray_offset is the global
+    index of the first ray (to key per-ray randomness).
+    Returns (rgb (n_frames,H,W,3), depth (n_frames,H,W)) on every rank.
+    """
+    world, rank = _world(group)
+    total = n_frames * H * W
+    start, end, per = shard_range(total, world, rank)
+    buf = torch.zeros(per, 4, device=device)
+    if end > start:
+        o, d = shard_rays(ray_fn, H, W, n_frames, start, end)
+        rgb, depth = render_fn(o, d, start)
+        buf[: end - start, :3] = rgb.to(buf.device)
+        buf[: end - start, 3:] = depth.reshape(-1, 1).to(buf.device)
+    if world > 1:
+        out = torch.empty(world * per, 4, device=buf.device)
+        dist.all_gather_into_tensor(out, buf, group=group)
+    else:
+        out = buf
+    frames = out[:total].reshape(n_frames, H, W, 4)
+    return frames[..., :3], frames[..., 3]
+
+
+def render_path_frames(model, poses, H, W, focal, near, far, n_samples, n_importance=0, appearance_embedding=None,
+                       perturb=False, hierarchical=False, seed=0, group=None, timing=None):
+    """render_frames_sharded with nerfmi's HIP get_rays / render_rays (one list entry per frame:
+    a (3,4)/(4,4) c2w).  timing: passed to render_rays (per-launch MLP events)."""
+    from . import _lib
+    from .ray_utils import get_rays
+    from .render import render_rays
+    dev = _lib.device()
+    c2ws = [torch.as_tensor(p, dtype=torch.float32) for p in poses]
+
+    def ray_fn(frame, row0, nrows):
+        o, d = get_rays(H, W, focal, c2ws[frame].to(dev), rows=(row0, nrows))
+        return o.reshape(-1, 3), d.reshape(-1, 3)
+
+    def render_fn(o, d, offset):
+        rgb, depth, _ = render_rays(model, o, d, near, far, n_samples, n_importance,
+                                    appearance_embedding=appearance_embedding, perturb=perturb,
+                                    hierarchical=hierarchical, seed=(seed * 1_000_003 + offset) & (2 ** 62 - 1),
+                                    timing=timing)
+        return rgb, depth
+
+    return render_frames_sharded(ray_fn, render_fn, H, W, len(c2ws), group=group, device=dev)

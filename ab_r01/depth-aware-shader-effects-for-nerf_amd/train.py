@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .models import NeRF, STATE_KEYS, state_tensors
+from .models import NeRF, STATE_KEYS
 from .ray_utils import linspace_table
 
 _APP_DIM = 32
@@ -49,11 +49,7 @@ class Trainer:
         self.group = group
         model = model if model is not None else NeRF(config)
         self.model = model.to(self.dev)
-        named = dict(self.model.named_parameters())
-        # 24 parameter slots in STATE_KEYS order; a use_appearance=False model has no
-        # appearance_projection (models.py:99-103): its slots stay zero and are not parameters
-        self.present = [k in named for k in STATE_KEYS]
-        tensors = state_tensors(named, self.dev)
+        tensors = [dict(self.model.named_parameters())[k] for k in STATE_KEYS]
         self.shapes = [tuple(t.shape) for t in tensors]
         self.sizes = [t.numel() for t in tensors]
         if config.use_appearance:
@@ -77,25 +73,10 @@ class Trainer:
                 self.view(self.flat, len(tensors)).copy_(appearance_embeddings.detach())
             # the module's parameters become views of the flat buffer
             for i, k in enumerate(STATE_KEYS):
-                if not self.present[i]:
-                    continue
                 mod_name, pname = k.rsplit(".", 1)
                 mod = self.model.get_submodule(mod_name)
                 setattr(mod, pname, torch.nn.Parameter(self.view(self.flat, i), requires_grad=False))
         self.appearance_embeddings = self.view(self.flat, len(tensors)) if self.n_images else None
-        if isinstance(appearance_embeddings, torch.nn.Parameter):
-            # the caller's table (dataset.appearance_embeddings, an nn.Parameter as dataset.py:81-83)
-            # becomes a view of the flat buffer, so every optimizer step updates it in place as
-            # the reference's Adam does (train.py:36-39)
-            appearance_embeddings.data = self.appearance_embeddings
-        # Adam's parameter numbering (model.parameters() order, then the appearance table)
-        self.param_slots = [i for i in range(24) if self.present[i]] + ([24] if self.n_images else [])
-        self.rank = 0
-        if group is not None:
-            import torch.distributed as dist
-            self.rank = dist.get_rank(group)
-        # every rank starts from rank 0's weights and table, as DDP's constructor does
-        broadcast_state([self.flat], group)
         self.param_ptrs = (ctypes.c_void_p * 24)(*[self.view(self.flat, i).data_ptr() for i in range(24)])
         self.grad_ptrs = (ctypes.c_void_p * 24)(*[self.view(self.grad, i).data_ptr() for i in range(24)])
         self.app_grad = self.view(self.grad, 24) if self.n_images else None
@@ -134,7 +115,7 @@ class Trainer:
             t_rand = t_rand.to(self.dev, torch.float32).contiguous()
             assert t_rand.shape == (B, N)
         if seed is None:
-            seed = step_seed(self.steps + 1, self.rank)
+            seed = self.steps + 1
         _lib.check(lib.nerf_pack_weights(self.param_ptrs, P(self.packed), s), "nerf_pack_weights")
         _lib.check(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), s),
                    "nerf_pack_weights_transposed")
@@ -182,8 +163,7 @@ class Trainer:
         dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
         feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save, grad = torch.empty(M, _lib.SAVE_ROW, device=dev), torch.empty(M, _lib.GRAD_ROW, device=dev)
-        masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev)
+        save, grad = torch.empty(M, 2400, device=dev), torch.empty(M, 2312, device=dev)
         rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
         dsig, drgb, sq = torch.empty(M, device=dev), torch.empty(M, 3, device=dev), torch.empty(B, device=dev)
         grads = [torch.empty_like(self.view(self.grad, i)) for i in range(24)]
@@ -206,15 +186,14 @@ class Trainer:
         ck(lib.nerf_ray_features_train(P(self.packed), P(dn), B, P(app), rows, P(feat), P(encd), s), "features")
         ev[2].record(cur)
         ck(lib.nerf_mlp_forward_train(P(self.packed), P(o), P(dn), P(z), B, N, P(feat), P(encd), P(rgb), P(sigma),
-                                      P(save), P(masks), s), "mlp_forward_train")
+                                      P(save), s), "mlp_forward_train")
         ev[3].record(cur)
         ck(lib.nerf_composite(P(rgb), P(sigma), P(z), B, N, P(rgb_map), P(depth), None, s), "composite")
         ck(lib.nerf_composite_backward(P(rgb), P(sigma), P(z), P(rgb_map), P(tgt), B, N, 2.0 / (3 * B), P(dsig),
                                        P(drgb), P(sq), s), "composite_backward")
         ev[4].record(cur)
-        mk = masks if _lib.get_mlp_arith() == "f16x3" else None    # the f16x3 forward wrote them
-        ck(lib.nerf_mlp_backward(P(self.packed), P(self.packedT), P(save), P(mk), P(sigma), P(rgb), P(dsig), P(drgb),
-                                 M, P(grad), s), "mlp_backward")
+        ck(lib.nerf_mlp_backward(P(self.packed), P(self.packedT), P(save), P(sigma), P(rgb), P(dsig), P(drgb), M,
+                                 P(grad), s), "mlp_backward")
         ev[5].record(cur)
         ck(lib.nerf_param_grads(P(save), P(grad), M, N, P(app), rows, P(self.packed), gptr, P(self.dapp), P(ws),
                                 wsz, s), "param_grads")
@@ -248,13 +227,13 @@ class Trainer:
     def optimizer_state_dict(self):
         """torch.optim.Adam.state_dict() layout (train.py:116,178): per-parameter step/exp_avg/exp_avg_sq,
         parameters numbered model.parameters() order then the appearance table."""
-        n = len(self.param_slots)
+        n = 24 + (1 if self.n_images else 0)
         state = {}
         if self.steps:
-            for i, slot in enumerate(self.param_slots):
+            for i in range(n):
                 state[i] = {"step": torch.tensor(float(self.steps)),
-                            "exp_avg": self.view(self.exp_avg, slot).detach().cpu().clone(),
-                            "exp_avg_sq": self.view(self.exp_avg_sq, slot).detach().cpu().clone()}
+                            "exp_avg": self.view(self.exp_avg, i).detach().cpu().clone(),
+                            "exp_avg_sq": self.view(self.exp_avg_sq, i).detach().cpu().clone()}
         group = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": 0, "amsgrad": False,
                  "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
                  "decoupled_weight_decay": False, "initial_lr": self.initial_lr, "params": list(range(n))}
@@ -262,16 +241,11 @@ class Trainer:
 
     def load_optimizer_state_dict(self, sd):
         st = sd["state"]
-        if len(sd["param_groups"][0]["params"]) != len(self.param_slots):
-            raise ValueError(f"optimizer state has {len(sd['param_groups'][0]['params'])} parameters, "
-                             f"this trainer {len(self.param_slots)}")
         for i, e in st.items():
-            slot = self.param_slots[int(i)]
-            self.view(self.exp_avg, slot).copy_(e["exp_avg"])
-            self.view(self.exp_avg_sq, slot).copy_(e["exp_avg_sq"])
+            self.view(self.exp_avg, int(i)).copy_(e["exp_avg"])
+            self.view(self.exp_avg_sq, int(i)).copy_(e["exp_avg_sq"])
             self.steps = int(float(e["step"]))
         self.lr = sd["param_groups"][0]["lr"]
-        broadcast_state([self.exp_avg, self.exp_avg_sq], self.group)
 
     def checkpoint(self, loss, psnr, iteration):
         """The dict train.py:114-125 saves."""
@@ -281,23 +255,6 @@ class Trainer:
         if self.n_images:
             ck["appearance_embeddings"] = self.appearance_embeddings.detach().cpu().clone()
         return ck
-
-
-def step_seed(key, rank):
-    """Key of a step's in-kernel jitter stream: distinct per step and per data-parallel rank (the
-    reference draws torch.rand per call, ray_utils.py:80; ranks must not share draws)."""
-    return (int(key) & ((1 << 40) - 1)) | (int(rank) << 40)
-
-
-def broadcast_state(tensors, group):
-    """Rank 0's copy of each tensor on every rank of `group` (a no-op alone)."""
-    if group is None:
-        return
-    import torch.distributed as dist
-    if dist.get_world_size(group) > 1:
-        src = dist.get_global_rank(group, 0)
-        for t in tensors:
-            dist.broadcast(t, src=src, group=group)
 
 
 def average_gradients(flat_grad, group):
@@ -315,15 +272,9 @@ def average_gradients(flat_grad, group):
 
 
 def train_nerf(config, dataset, save_dir="checkpoints", group=None, num_iterations=None, log_every=10,
-               checkpoint_every=1000, seed=None, plots=True, return_metrics=False):
-    """src/train.py:13-207 on nerfmi: returns the trained model, as the reference does
-    (train.py:207; run.py:347 assigns it).  ``return_metrics=True`` returns (model, losses, psnrs)
-    instead; the per-iteration losses and PSNRs are also left on ``train_nerf.losses`` /
-    ``train_nerf.psnrs``.  The dataset's appearance table (an nn.Parameter, dataset.py:81-83) is
-    trained in place (train.py:36-39).  Every ``checkpoint_every`` iterations rank 0 writes
-    checkpoint_{i:06d}.pt and the validation render render_{i:06d}.png of train.py:127-173.
-    Under data parallelism every rank draws its own batch (its own image, its own jitter
-    stream) and the gradients are averaged; rank 0 writes."""
+               checkpoint_every=1000, seed=None, plots=True):
+    """src/train.py:13-207 on nerfmi: returns (model, losses, psnrs).  Under data parallelism every
+    rank draws its own batch (its own image) and the gradients are averaged; rank 0 writes."""
     import torch.distributed as dist
     rank = dist.get_rank(group) if group is not None else 0
     if rank == 0:
@@ -333,14 +284,13 @@ def train_nerf(config, dataset, save_dir="checkpoints", group=None, num_iteratio
                       n_images=len(dataset), group=group)
     iters = config.num_iterations if num_iterations is None else num_iterations
     losses, psnrs = [], []
-    train_nerf.losses, train_nerf.psnrs = losses, psnrs
     start = time.time()
     loss_v = psnr_v = float("nan")
     for i in range(1, iters + 1):
         batch = dataset.get_rays(batch_size=initial_batch_size) if i <= 5 else dataset.get_rays()
         app_idx = batch["appearance_idx"] if config.use_appearance else None
         loss = trainer.step(batch["rays_o"], batch["rays_d"], batch["rgb"], app_idx,
-                            seed=None if seed is None else step_seed(seed * 1_000_003 + i, trainer.rank))
+                            seed=None if seed is None else seed * 1_000_003 + i)
         if i % config.scheduler_step_size == 0:                          # StepLR, train.py:95-96
             trainer.lr *= config.scheduler_gamma
         loss_v = float(loss)
@@ -351,49 +301,12 @@ def train_nerf(config, dataset, save_dir="checkpoints", group=None, num_iteratio
             print(f"iter {i}: Loss: {loss_v:.5f}, PSNR: {psnr_v:.2f}")
         if rank == 0 and checkpoint_every and i % checkpoint_every == 0:
             torch.save(trainer.checkpoint(loss_v, psnr_v, i), os.path.join(save_dir, f"checkpoint_{i:06d}.pt"))
-            if plots:
-                validation_render(trainer.model, dataset, config, i, save_dir)
     if rank == 0:
         torch.save(trainer.checkpoint(loss_v, psnr_v, iters), os.path.join(save_dir, "checkpoint_final.pt"))
         if plots:
             _plot_curves(losses, psnrs, os.path.join(save_dir, "training_curves.png"))
         print(f"Training completed in {time.time() - start:.2f}s")
-    if return_metrics:
-        return trainer.model, losses, psnrs
-    return trainer.model
-
-
-@torch.no_grad()
-def validation_render(model, dataset, config, iteration, save_dir):
-    """The sample render of train.py:127-173: the first 1000 rays of the last image, coarse
-    volume_render with perturb=False, RGB and viridis depth side by side in
-    render_{iteration:06d}.png.  Returns (rgb (1000,3), depth (1000,1))."""
-    from .render import volume_render
-    val = dataset.get_rays(idx=len(dataset) - 1)
-    o, d = val["rays_o"][:1000], val["rays_d"][:1000]
-    app = None
-    if config.use_appearance:
-        app = dataset.appearance_embeddings[val["appearance_idx"]]
-    rgb, depth, _ = volume_render(model, o, d, near=dataset.near, far=dataset.far, n_samples=config.num_samples,
-                                  n_importance=config.num_importance, appearance_embedding=app, perturb=False)
-    import matplotlib
-    matplotlib.use("Agg")
-    import matplotlib.pyplot as plt
-    rgb_viz = rgb.reshape(-1, 3).cpu().numpy()
-    n = int(np.sqrt(rgb_viz.shape[0]))
-    plt.figure(figsize=(10, 5))
-    plt.subplot(1, 2, 1)
-    plt.imshow(np.clip(rgb_viz[:n * n].reshape(n, n, 3), 0, 1))
-    plt.title(f"RGB - Iteration {iteration}")
-    plt.axis("off")
-    plt.subplot(1, 2, 2)
-    plt.imshow(depth.reshape(-1).cpu().numpy()[:n * n].reshape(n, n), cmap="viridis")
-    plt.title(f"Depth - Iteration {iteration}")
-    plt.colorbar()
-    plt.axis("off")
-    plt.savefig(os.path.join(save_dir, f"render_{iteration:06d}.png"))
-    plt.close()
-    return rgb, depth
+    return trainer.model, losses, psnrs
 
 
 def _plot_curves(losses, psnrs, path):

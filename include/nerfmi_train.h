@@ -29,7 +29,7 @@ extern "C" {
 #define NERF_SAVE_ROW 2400 /* [h0..h3 | enc_x(64) | h4..h7 | enc_d(32) | r_dir(128) | hd(128)] */
 #define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dhd(128) | drgb(3)+pad | dsigma+pad] */
 /* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):
- * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes. */
+ * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes (csrc/layout.h kMaskRow). */
 #define NERF_MASK_ROW 68
 
 /* ---------------------------------------------------------------- whole step
@@ -71,9 +71,9 @@ int nerf_composite_backward(const float* rgb, const float* sigma, const float* z
                             const float* rgb_map, const float* target, int64_t B, int N,
                             float scale, float* dsigma, float* drgb, float* sq_err,
                             nerf_stream_t stream);
-/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW).  The ReLU
- * masks come from `masks` when non-null (the f16x3 forward's; same arithmetic on both sides), else
- * from the saved activations. */
+/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW).  Under
+ * f16x3 the ReLU masks come from `masks` when non-null (an f16x3 forward's), else from the saved
+ * activations; the f32 backward always reads the activations. */
 int nerf_mlp_backward(const float* packed, const float* packedT, const float* save,
                       const uint32_t* masks, const float* sigma, const float* rgb,
                       const float* dsigma, const float* drgb, int64_t M, float* grad,
