@@ -899,7 +899,10 @@ __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int WN, int WK>
+// XD1 (x_div == 1, one x row per sample: every trunk/head layer): the loader's per-sample offsets
+// are stage-invariant VGPRs and only the buffer descriptors move per stage (no VALU address work;
+// the generic x path divides and carries per sample, ~130 VALU per stage).
+template <int WN, int WK, bool XD1>
 __global__ void __launch_bounds__(256, WN == 4 ? 1 : 2)   // 256 x 64 tiles: 94 KB of LDS, one block per CU
 wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
                 int64_t x_div, int64_t M, int ntk, int tiles, int chunks, int clen, float* __restrict__ partial) {
@@ -921,7 +924,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   const int64_t m1 = m0 + clen < M ? m0 + clen : M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wn = w % WN, wk = w / WN;
-  float ra[SA][8], rx[SX][8];
+  float ra[2][SA][8], rx[2][SX][8];   // two stages in flight: stage k's values in set k % 2
   float bacc[SA];
 #pragma unroll
   for (int q = 0; q < SA; ++q) bacc[q] = 0.0f;
@@ -945,6 +948,20 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
     const int slot = tid + 256 * q, col = slot % BK;
     xcol[q] = (slot < 2 * BK && k0 + col < K) ? 4u * (uint32_t)(k0 + col) : kOut;
   }
+  uint32_t avo[SA][8], xvo[SX][8];   // XD1: sample j of a slot at a stage-invariant offset
+#pragma unroll
+  for (int q = 0; q < SA; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) avo[q][j] = aoff[q] == kOut ? kOut : aoff[q] + (uint32_t)j * lda4;
+  if constexpr (XD1) {
+#pragma unroll
+    for (int q = 0; q < SX; ++q) {
+      const int oct = (tid + 256 * q) / BK;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        xvo[q][j] = xcol[q] == kOut ? kOut : (uint32_t)(8 * oct + j) * ldx4 + xcol[q];
+    }
+  }
   const uint32_t xd = x_div == 0 ? 0xFFFFFFFFu : (uint32_t)x_div;
   const int64_t xr0 = x_div == 0 ? 0 : m0 / x_div;
   const uint32_t r0 = x_div == 0 ? 0u : (uint32_t)(m0 - xr0 * x_div);
@@ -952,7 +969,9 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(x + xr0 * ldx), (short)0, (int)(xrows * ldx4), 0x00020000);
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  auto load = [&](int stage) __attribute__((always_inline)) {
+  // stage `stage` (< nstages) into register set SET; past the last stage it loads nothing
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage);
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
@@ -960,7 +979,17 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
     for (int q = 0; q < SA; ++q)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        ra[q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)(aoff[q] + j * lda4), 0, 0));
+        ra[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[q][j], 0, 0));
+    if constexpr (XD1) {
+      const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+#pragma unroll
+      for (int q = 0; q < SX; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xs, (int)xvo[q][j], 0, 0));
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < SX; ++q) {
       const int slot = tid + 256 * q, oct = slot / BK;
@@ -970,7 +999,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
       for (int j = 0; j < 8; ++j) {
         const bool ok = rel + j < mrel_end && xcol[q] != kOut;
         const uint32_t off = ok ? row * ldx4 + xcol[q] : kOut;
-        rx[q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)off, 0, 0));
+        rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)off, 0, 0));
         if (++r == xd) {
           r = 0;
           ++row;
@@ -994,35 +1023,44 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
     *reinterpret_cast<bf16x8*>(&dst[col + plane_stride][8 * oct]) = p1;
     *reinterpret_cast<bf16x8*>(&dst[col + 2 * plane_stride][8 * oct]) = p2;
   };
-  auto store = [&](int buf) __attribute__((always_inline)) {
+  auto store = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
 #pragma unroll
     for (int q = 0; q < SA; ++q) {
       const int slot = tid + 256 * q, col = slot % BN, oct = slot / BN;
       if (slot < 2 * BN) {
         if (do_bias) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bacc[q] += ra[q][j];
+          for (int j = 0; j < 8; ++j) bacc[q] += ra[SET][q][j];
         }
-        split_store(ra[q], &As[buf][0][0], col, oct, BN);
+        split_store(ra[SET][q], &As[buf][0][0], col, oct, BN);
       }
     }
 #pragma unroll
     for (int q = 0; q < SX; ++q) {
       const int slot = tid + 256 * q, col = slot % BK, oct = slot / BK;
-      if (slot < 2 * BK) split_store(rx[q], &Xs[buf][0][0], col, oct, BK);
+      if (slot < 2 * BK) split_store(rx[SET][q], &Xs[buf][0][0], col, oct, BK);
     }
   };
   const bool n_act0 = n0 + 64 * wn < N, n_act1 = n0 + 64 * wn + 32 < N;
   const bool k_act0 = k0 + 64 * wk < K, k_act1 = k0 + 64 * wk + 32 < K;
   f32x16 acc[2][2] = {{f32x16{}, f32x16{}}, {f32x16{}, f32x16{}}};
   const int nstages = (int)((m1 - m0 + kBfStage - 1) / kBfStage);
-  load(0);
-  store(0);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  // Loads run two stages ahead of the MFMAs: iteration st issues stage st+2's loads, splits stage
+  // st+1's values (loaded a whole iteration earlier) into the other LDS buffer, and runs stage st's
+  // MFMAs.  (One stage ahead, the split waited on loads issued only one MFMA stage before.)
+  load(S0{}, 0);
+  if (nstages > 1) load(S1{}, 1);
+  store(S0{}, 0);
   __syncthreads();
   const int h = lane >> 5, c = lane & 31;
-  for (int st = 0; st < nstages; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nstages) load(st + 1);
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;            // st % 2
+    using Other = std::integral_constant<int, 1 - SET>;
+    const int buf = SET;
+    if (st + 2 < nstages) load(set_c, st + 2);
     if (n_act0 && k_act0) {
       bf16x8 fa[2][3], fx[2][3];
 #pragma unroll
@@ -1047,8 +1085,12 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
           acc[i][j] = mfma_bf16(fa[i][0], fx[j][0], t);
         }
     }
-    if (st + 1 < nstages) store(buf ^ 1);
+    if (st + 1 < nstages) store(Other{}, buf ^ 1);
     __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 2) {
+    iteration(S0{}, st);
+    if (st + 1 < nstages) iteration(S1{}, st + 1);
   }
   const int KP = K + 1;
   float* out = partial + (size_t)chunk * wgrad_stride(N, K);
@@ -1081,8 +1123,12 @@ static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, i
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
-  hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div,
-                     M, ntk, tiles, chunks, clen, ws);
+  if (x_div == 1)
+    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, true>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K,
+                       x_div, M, ntk, tiles, chunks, clen, ws);
+  else
+    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, false>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx,
+                       K, x_div, M, ntk, tiles, chunks, clen, ws);
   return check_launch("wgrad_bf_kernel");
 }
 

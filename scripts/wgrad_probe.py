@@ -1,0 +1,29 @@
+"""Standalone weight-gradient launch for profiling (rocprofv3 PMC / kernel stats): nerf_wgrad on
+the training step's hidden-layer shape (262,144 samples x 256 x 256, rows of the gradient and
+activation buffers as in the training workspace), ITERS launches."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nerfmi import _lib as L  # noqa: E402
+
+M, N, K = 262144, 256, 256
+ITERS = int(os.environ.get("ITERS", "20"))
+lib, dev = L.load(), L.device()
+g = torch.Generator(device=dev).manual_seed(0)
+a = torch.randn(M, L.GRAD_ROW, device=dev, generator=g)
+x = torch.randn(M, L.SAVE_ROW, device=dev, generator=g)
+ow, ob = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+ws = torch.empty(lib.nerf_wgrad_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
+for i in range(ITERS + 2):
+    if i == 2:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+    L.check(lib.nerf_wgrad(L.ptr(a), L.GRAD_ROW, N, L.ptr(x), L.SAVE_ROW, K, 1, M, L.ptr(ow), L.ptr(ob), 0, L.ptr(ws),
+                           ws.numel(), L.stream()), "wgrad")
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / ITERS
+print(f"wgrad {M}x{N}x{K}: {dt * 1e3:.3f} ms/launch, {2 * M * N * (K + 1) / dt / 1e12:.1f} TFLOP/s")
