@@ -128,21 +128,42 @@ __global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restric
 }
 
 // One block per layer: its scale, bound constants (layout.h).
+// Layer statistics for the split scales, one wave per row (lanes over the row's columns, so the
+// loads are coalesced): the row's max |W| and L1 norm, and |bias|, combined over the layer by
+// atomicMax on the float bits (non-negative floats order as unsigned integers: exact in any
+// order).  The raw maxima land in the constants' own slots (zeroed first) and
+// scale16_finalize_kernel turns them into the constants.
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
-  const int L = blockIdx.x;
-  float mx = 0.0f, l1 = 0.0f, bm = 0.0f;
-  if ((int)threadIdx.x < layer_rows(L)) layer_row_stats(P.p, L, threadIdx.x, mx, l1, bm);
-  __shared__ float red[3][256];
-  red[0][threadIdx.x] = mx;
-  red[1][threadIdx.x] = l1;
-  red[2][threadIdx.x] = bm;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w)
-      for (int q = 0; q < 3; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + w]);
-    __syncthreads();
+  const int L = blockIdx.y;
+  const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= layer_rows(L)) return;
+  float mx = 0.0f, l1 = 0.0f;
+  for (int c = lane; c < layer_cols(L); c += 64) {
+    const float w = fabsf(layer_weight(P.p, L, row, c));
+    mx = fmaxf(mx, w);
+    l1 += w;
   }
-  if (threadIdx.x == 0) store_layer_consts(packed + kOffScale16, L, red[0][0], red[1][0], red[2][0]);
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+    l1 += __shfl_xor(l1, off);
+  }
+  if (lane == 0) {
+    unsigned* cw = reinterpret_cast<unsigned*>(packed + kOffScale16);
+    atomicMax(cw + kS16Sw + L, __float_as_uint(mx));
+    if (L < 8) {
+      atomicMax(cw + kS16R + L, __float_as_uint(l1));
+      atomicMax(cw + kS16B + L, __float_as_uint(fabsf(P.p[2 * L + 1][row])));
+    }
+  }
+}
+
+__global__ void scale16_finalize_kernel(float* __restrict__ packed) {
+  const int L = threadIdx.x;
+  if (L >= kS16Layers) return;
+  float* consts = packed + kOffScale16;
+  const float mx = consts[kS16Sw + L];
+  const float l1 = L < 8 ? consts[kS16R + L] : 0.0f, bm = L < 8 ? consts[kS16B + L] : 0.0f;
+  store_layer_consts(consts, L, mx, l1, bm);
 }
 
 __global__ void __launch_bounds__(256) pack16_kernel(ParamPtrs P, float* __restrict__ packed) {
@@ -158,8 +179,10 @@ int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   if (int rc = check_launch("pack_kernel")) return rc;
   if (hipMemsetAsync(packed + kOffScale16, 0, kS16Consts * sizeof(float), s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "pack: hipMemsetAsync failed");
-  hipLaunchKernelGGL(scale16_kernel, dim3(kS16Layers), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(scale16_kernel, dim3(kHidden / 4, kS16Layers), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("scale16_kernel")) return rc;
+  hipLaunchKernelGGL(scale16_finalize_kernel, dim3(1), dim3(64), 0, s, packed);
+  if (int rc = check_launch("scale16_finalize_kernel")) return rc;
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((kFragFloats + 255) / 256)), dim3(256), 0, s, P, packed);
   return check_launch("pack16_kernel");
 }

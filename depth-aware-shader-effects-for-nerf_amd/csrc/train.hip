@@ -230,16 +230,23 @@ __global__ void __launch_bounds__(256) packT_kernel(ParamPtrsT P, float* __restr
   if (e < kPackedT32Floats) packed[e] = packT_value(P.p, e);
 }
 
-// one block per matrix: s_w and 1/s_w
+// max |W^T| of matrix mt (= max |W| over its columns i < kHidden), 8 rows of W^T per block
+// (thread = row i, coalesced over i), combined by atomicMax on the float bits (exact in any order)
+// into consts[mt] (zeroed first); scaleT16_finalize_kernel turns the maxima into s_w and 1/s_w.
 __global__ void __launch_bounds__(256) scaleT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
-  __shared__ float red[256];
-  red[threadIdx.x] = tmat_row_max(P.p, blockIdx.x, threadIdx.x);
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) store_t16_consts(packed + kOffT16Consts, blockIdx.x, red[0]);
+  const int mt = blockIdx.y, i = threadIdx.x;
+  const int outs = mt == 7 ? kDirHidden : kHidden;
+  const int o0 = blockIdx.x * 8;
+  float m = 0.0f;
+  for (int o = o0; o < o0 + 8 && o < outs; ++o) m = fmaxf(m, fabsf(tmat_weight(P.p, mt, i, o)));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(reinterpret_cast<unsigned*>(packed + kOffT16Consts) + mt, __float_as_uint(m));
+}
+
+__global__ void scaleT16_finalize_kernel(float* __restrict__ packed) {
+  const int mt = threadIdx.x;
+  if (mt < 8) store_t16_consts(packed + kOffT16Consts, mt, packed[kOffT16Consts + mt]);
 }
 
 __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
@@ -253,8 +260,12 @@ int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
   hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256)), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("packT_kernel")) return rc;
-  hipLaunchKernelGGL(scaleT16_kernel, dim3(8), dim3(256), 0, s, P, packedT);
+  if (hipMemsetAsync(packedT + kOffT16Consts, 0, 8 * sizeof(float), s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "packT: hipMemsetAsync failed");
+  hipLaunchKernelGGL(scaleT16_kernel, dim3(kHidden / 8, 8), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("scaleT16_kernel")) return rc;
+  hipLaunchKernelGGL(scaleT16_finalize_kernel, dim3(1), dim3(64), 0, s, packedT);
+  if (int rc = check_launch("scaleT16_finalize_kernel")) return rc;
   const size_t words = kOffT16Consts - kPackedT32Floats;
   hipLaunchKernelGGL(packT16_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, packedT);
   return check_launch("packT16_kernel");
@@ -696,7 +707,9 @@ constexpr int kWChunk = 2048;   // samples per chunk
 // and the appearance projection) hold one block per CU and have one tile: 1024-sample chunks give
 // 256 blocks instead of 128.  The 128x128-tile launches hold two blocks per CU; those with fewer
 // than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
+static inline bool wgrad_whole_tile(int N, int K) { return N == 256 && K == 256; }
 static inline int wgrad_chunk_len(int N, int K) {
+  if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
   if (K <= 64 && N > 64) return kWChunk / 2;
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
   return tiles == 1 ? kWChunk / 4 : tiles == 2 ? kWChunk / 2 : kWChunk;
@@ -1117,6 +1130,125 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   }
 }
 
+// The 256 x 256 trunk layers (N = K = 256, one x row per sample): the whole weight gradient of a
+// chunk in one workgroup of 8 waves (2 per SIMD), each wave a 128 (n) x 64 (k) sub-tile (4 x 2
+// MFMA tiles).  Against wgrad_bf_kernel's 128 x 128 tiles every operand value is split into its
+// bf16 parts once instead of twice, and a wave reads 0.375 instead of 0.5 KiB of LDS fragments per
+// MFMA.  Same arithmetic (bf16x6), same partial layout and deterministic chunk reduction.
+// LDS: 2 buffers x 3 parts x (256 + 256) rows x 48 bytes = 147 KiB: one workgroup per CU.
+// (Tried and dropped, same-box A/B: loads two stages ahead with the split interleaved between the
+// MFMAs (spills at 2 waves per SIMD), and 4 waves of 128 x 128 with 256 accumulators (-18 %).)
+constexpr int kWT = 256;
+__global__ void __launch_bounds__(512, 1)
+wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
+                   int clen, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][kWT][kBfRow];
+  __shared__ float bsum[2][kWT];
+  const int chunk = blockIdx.x;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wn = w & 1, wk = w >> 1;                 // n rows 128 wn .., k columns 64 wk ..
+  // loader: thread tid owns column tid % 256, samples 8 (tid / 256) .. +7 of each 16-sample stage
+  const int col = tid % kWT, oct = tid / kWT;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  uint32_t avo[8], xvo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    avo[j] = (uint32_t)(8 * oct + j) * lda4 + 4u * (uint32_t)col;
+    xvo[j] = (uint32_t)(8 * oct + j) * ldx4 + 4u * (uint32_t)col;
+  }
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[8], rx[8];
+  float bacc = 0.0f;
+  auto load = [&](int stage) __attribute__((always_inline)) {
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage);
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ra[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[j], 0, 0));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rx[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[j], 0, 0));
+  };
+  auto split_store = [&](const float (&v)[8], __bf16 (*dst)[kBfRow]) __attribute__((always_inline)) {
+    bf16x8 p0, p1, p2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 h0 = (__bf16)v[j];
+      const float r1 = v[j] - (float)h0;
+      const __bf16 h1 = (__bf16)r1;
+      const float r2 = r1 - (float)h1;
+      p0[j] = h0;
+      p1[j] = h1;
+      p2[j] = (__bf16)r2;
+    }
+    *reinterpret_cast<bf16x8*>(&dst[col][8 * oct]) = p0;
+    *reinterpret_cast<bf16x8*>(&dst[col + kWT][8 * oct]) = p1;
+    *reinterpret_cast<bf16x8*>(&dst[col + 2 * kWT][8 * oct]) = p2;
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bacc += ra[j];
+    split_store(ra, &As[buf][0][0]);
+    split_store(rx, &Xs[buf][0][0]);
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  const int nstages = (int)((m1 - m0 + kBfStage - 1) / kBfStage);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int h = lane >> 5, c = lane & 31;
+  for (int st = 0; st < nstages; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nstages) load(st + 1);
+    bf16x8 fx[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fx[j][p] = *reinterpret_cast<const bf16x8*>(&Xs[buf][p][64 * wk + 32 * j + c][8 * h]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[buf][p][128 * wn + 32 * i + c][8 * h]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma_bf16(fa[0], fx[j][2], t);
+        t = mfma_bf16(fa[1], fx[j][1], t);
+        t = mfma_bf16(fa[2], fx[j][0], t);
+        t = mfma_bf16(fa[0], fx[j][1], t);
+        t = mfma_bf16(fa[1], fx[j][0], t);
+        acc[i][j] = mfma_bf16(fa[0], fx[j][0], t);
+      }
+    }
+    if (st + 1 < nstages) store(buf ^ 1);
+    __syncthreads();
+  }
+  constexpr int KP = kWT + 1;
+  float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = 64 * wk + 32 * j + c;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int nn = 128 * wn + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        out[(size_t)nn * KP + kk] = acc[i][j][g];
+      }
+    }
+  // bias column: every staged a value passed through store() exactly once
+  bsum[oct][col] = bacc;
+  __syncthreads();
+  if (tid < kWT) out[(size_t)tid * KP + kWT] = bsum[0][tid] + bsum[1][tid];
+}
+
 template <int WN, int WK>
 static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
                            int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
@@ -1201,7 +1333,10 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K);
     chunks = (int)((M + clen - 1) / clen);
-    if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+    if (wgrad_whole_tile(N, K) && x_div == 1) {
+      hipLaunchKernelGGL(wgrad_bf256_kernel, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
+      rc = check_launch("wgrad_bf256_kernel");
+    } else if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
     else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
   } else if (aligned && K >= 1 && K <= 64 && N > 64)
     rc = launch_wgrad_lds<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
