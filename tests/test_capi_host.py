@@ -53,7 +53,7 @@ def test_bad_arguments_are_reported_not_launched():
     assert lib.nerf_adam(None, None, None, None, 8, 1e-3, .9, .999, 1e-8, 0, None) == 1   # step counts from 1
     assert lib.nerf_wgrad(None, 1, 4, None, 4, 4, 1, 8, None, None, 0, None, 0, None) == 1
     ws = lib.nerf_wgrad_workspace_bytes(5000, 256, 256)
-    assert ws == 3 * 256 * 257 * 4                      # 2048-sample chunks x N x (K + bias column)
+    assert ws == 5 * 256 * 257 * 4        # 1024-sample chunks (the 256 x 256 path) x N x (K + bias column)
     assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2312) * 4
     assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, None, 0, None, None) == 0
     # post effects
