@@ -510,3 +510,19 @@ int main() {
                     str(src), "-o", str(exe)], check=True)
     worst = float(subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout)
     assert worst < 1.6e-7, worst
+
+
+@pytest.mark.skipif(os.environ.get("NERFMI_SANITIZED") == "1", reason="already the sanitized run")
+def test_host_abi_under_asan_ubsan():
+    """The host tests above, against the ASan + UBSan build of the C ABI (host code only;
+    scripts/sanitize_host.sh): argument checks, workspace carving and the host packers run with
+    every access and every undefined-behaviour check instrumented."""
+    import shutil
+    import subprocess
+    if not shutil.which("make") or not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc to build the sanitized library")
+    r = subprocess.run(["bash", os.path.join(REPO, "scripts", "sanitize_host.sh")], capture_output=True, text=True,
+                       timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "AddressSanitizer" not in out and "runtime error" not in out, out[-3000:]
