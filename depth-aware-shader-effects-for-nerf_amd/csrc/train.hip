@@ -1160,18 +1160,24 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
     xvo[j] = (uint32_t)(8 * oct + j) * ldx4 + 4u * (uint32_t)col;
   }
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[8], rx[8];
+  float ra[2][8], rx[2][8];   // two stages in flight: stage k's values in set k % 2
   float bacc = 0.0f;
-  auto load = [&](int stage) __attribute__((always_inline)) {
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage);
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    // a stage past the chunk's end gets empty resources (its loads read 0): the loads are issued
+    // unconditionally, so the compiler's vmcnt for the older set counts them (a conditional load
+    // makes it wait for everything)
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ra[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[j], 0, 0));
+    for (int j = 0; j < 8; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[j], 0, 0));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rx[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[j], 0, 0));
+    for (int j = 0; j < 8; ++j)
+      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[j], 0, 0));
   };
   auto split_store = [&](const float (&v)[8], __bf16 (*dst)[kBfRow]) __attribute__((always_inline)) {
     bf16x8 p0, p1, p2;
@@ -1189,23 +1195,32 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
     *reinterpret_cast<bf16x8*>(&dst[col + kWT][8 * oct]) = p1;
     *reinterpret_cast<bf16x8*>(&dst[col + 2 * kWT][8 * oct]) = p2;
   };
-  auto store = [&](int buf) __attribute__((always_inline)) {
+  auto store = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += ra[j];
-    split_store(ra, &As[buf][0][0]);
-    split_store(rx, &Xs[buf][0][0]);
+    for (int j = 0; j < 8; ++j) bacc += ra[SET][j];
+    split_store(ra[SET], &As[buf][0][0]);
+    split_store(rx[SET], &Xs[buf][0][0]);
   };
   f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
   const int nstages = (int)((m1 - m0 + kBfStage - 1) / kBfStage);
-  load(0);
-  store(0);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(S0{}, 0);
+  if (nstages > 1) load(S1{}, 1);
+  store(S0{}, 0);
   __syncthreads();
   const int h = lane >> 5, c = lane & 31;
-  for (int st = 0; st < nstages; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nstages) load(st + 1);
+  // iteration st: stage st+2's loads into the set stage st vacated, stage st's MFMAs, stage st+1's
+  // split (its loads issued a whole iteration earlier) into the other LDS buffer
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    using Other = std::integral_constant<int, 1 - SET>;
+    const int buf = SET;
+    load(set_c, st + 2);
+    __builtin_amdgcn_sched_barrier(0);   // issued first: the split below waits only for the older set
     bf16x8 fx[2][3];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
@@ -1227,8 +1242,12 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         acc[i][j] = mfma_bf16(fa[0], fx[j][0], t);
       }
     }
-    if (st + 1 < nstages) store(buf ^ 1);
+    if (st + 1 < nstages) store(Other{}, buf ^ 1);
     __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 2) {
+    iteration(S0{}, st);
+    if (st + 1 < nstages) iteration(S1{}, st + 1);
   }
   constexpr int KP = kWT + 1;
   float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
