@@ -1132,41 +1132,54 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
 
 // The 256 x 256 trunk layers (N = K = 256, one x row per sample): the whole weight gradient of a
 // chunk in one workgroup of 8 waves (2 per SIMD), each wave a 128 (n) x 64 (k) sub-tile (4 x 2
-// MFMA tiles).  Against wgrad_bf_kernel's 128 x 128 tiles every operand value is split into its
-// bf16 parts once instead of twice, and a wave reads 0.375 instead of 0.5 KiB of LDS fragments per
-// MFMA.  Same arithmetic (bf16x6), same partial layout and deterministic chunk reduction.
-// LDS: 2 buffers x 3 parts x (256 + 256) rows x 48 bytes = 147 KiB: one workgroup per CU.
-// (Tried and dropped, same-box A/B: loads two stages ahead with the split interleaved between the
-// MFMAs (spills at 2 waves per SIMD), and 4 waves of 128 x 128 with 256 accumulators (-18 %).)
+// MFMA tiles).  Same arithmetic (bf16x6), same partial layout and deterministic chunk reduction as
+// wgrad_bf_kernel.
+//   x (the B operand: column k, samples 8h .. 8h+7 in lane (k & 31) + 32h) is loaded by each wave
+//   straight in fragment order and split in registers: the two waves of a k range each split it,
+//   and it never touches LDS.
+//   a (the A operand, shared by the four waves of an n half) goes through LDS, split once by the
+//   whole workgroup (thread: one column, 8 samples) into [part][column][sample] rows of 48 bytes.
+// LDS traffic per 16-sample stage: 24 KiB written + 96 KiB of fragment reads (staging x as well
+// cost 48 + 144 KiB, and the MFMAs waited on it).  Loads run two stages ahead, issued
+// unconditionally (a stage past the chunk reads zeros through an empty buffer resource) so the
+// compiler's vmcnt waits count only the older stage.
 constexpr int kWT = 256;
+__device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h0 = (__bf16)v[j];
+    const float r1 = v[j] - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;
+    p0[j] = h0;
+    p1[j] = h1;
+    p2[j] = (__bf16)r2;
+  }
+}
 __global__ void __launch_bounds__(512, 1)
 wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
                    int clen, float* __restrict__ partial) {
   __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][kWT][kBfRow];
   __shared__ float bsum[2][kWT];
   const int chunk = blockIdx.x;
   const int64_t m0 = (int64_t)chunk * clen;
   const int64_t m1 = m0 + clen < M ? m0 + clen : M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wn = w & 1, wk = w >> 1;                 // n rows 128 wn .., k columns 64 wk ..
-  // loader: thread tid owns column tid % 256, samples 8 (tid / 256) .. +7 of each 16-sample stage
+  const int h = lane >> 5, c = lane & 31;
+  // a loader: thread tid owns column tid % 256, samples 8 (tid / 256) .. +7 of each stage; sample j
+  // of the octet at voffset avo + soffset j * lda4 (wave-uniform)
   const int col = tid % kWT, oct = tid / kWT;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  uint32_t avo[8], xvo[8];
+  const uint32_t avo = (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)col;
+  uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    avo[j] = (uint32_t)(8 * oct + j) * lda4 + 4u * (uint32_t)col;
-    xvo[j] = (uint32_t)(8 * oct + j) * ldx4 + 4u * (uint32_t)col;
-  }
+  for (int t = 0; t < 2; ++t) xvo[t] = (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)(64 * wk + 32 * t + c);
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[2][8], rx[2][8];   // two stages in flight: stage k's values in set k % 2
+  float ra[2][8], rx[2][2][8];   // two stages in flight: stage k's values in set k % 2
   float bacc = 0.0f;
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
-    // a stage past the chunk's end gets empty resources (its loads read 0): the loads are issued
-    // unconditionally, so the compiler's vmcnt for the older set counts them (a conditional load
-    // makes it wait for everything)
     const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
@@ -1174,58 +1187,46 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[j], 0, 0));
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * lda4), 0));
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[j], 0, 0));
-  };
-  auto split_store = [&](const float (&v)[8], __bf16 (*dst)[kBfRow]) __attribute__((always_inline)) {
-    bf16x8 p0, p1, p2;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const __bf16 h0 = (__bf16)v[j];
-      const float r1 = v[j] - (float)h0;
-      const __bf16 h1 = (__bf16)r1;
-      const float r2 = r1 - (float)h1;
-      p0[j] = h0;
-      p1[j] = h1;
-      p2[j] = (__bf16)r2;
-    }
-    *reinterpret_cast<bf16x8*>(&dst[col][8 * oct]) = p0;
-    *reinterpret_cast<bf16x8*>(&dst[col + kWT][8 * oct]) = p1;
-    *reinterpret_cast<bf16x8*>(&dst[col + 2 * kWT][8 * oct]) = p2;
+      for (int j = 0; j < 8; ++j)
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * ldx4), 0));
   };
-  auto store = [&](auto set_c, int buf) __attribute__((always_inline)) {
+  auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
 #pragma unroll
     for (int j = 0; j < 8; ++j) bacc += ra[SET][j];
-    split_store(ra[SET], &As[buf][0][0]);
-    split_store(rx[SET], &Xs[buf][0][0]);
+    bf16x8 p0, p1, p2;
+    split3_bf16(ra[SET], p0, p1, p2);
+    *reinterpret_cast<bf16x8*>(&As[buf][0][col][8 * oct]) = p0;
+    *reinterpret_cast<bf16x8*>(&As[buf][1][col][8 * oct]) = p1;
+    *reinterpret_cast<bf16x8*>(&As[buf][2][col][8 * oct]) = p2;
   };
   f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  const int nstages = (int)((m1 - m0 + kBfStage - 1) / kBfStage);
+  // an even number of stages (one past the chunk reads zeros): no conditional code in the loop, so
+  // the compiler's vmcnt waits see one pattern of loads
+  const int nstages = (int)((m1 - m0 + 2 * kBfStage - 1) / (2 * kBfStage)) * 2;
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   load(S0{}, 0);
-  if (nstages > 1) load(S1{}, 1);
-  store(S0{}, 0);
+  load(S1{}, 1);
+  store_a(S0{}, 0);
   __syncthreads();
-  const int h = lane >> 5, c = lane & 31;
-  // iteration st: stage st+2's loads into the set stage st vacated, stage st's MFMAs, stage st+1's
-  // split (its loads issued a whole iteration earlier) into the other LDS buffer
+  // iteration st: split stage st's x (set st % 2) into fragments, reuse the set for stage st+2's
+  // loads, stage st's MFMAs (a from LDS buffer st % 2), stage st+1's a into the other buffer
   auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     using Other = std::integral_constant<int, 1 - SET>;
     const int buf = SET;
-    load(set_c, st + 2);
-    __builtin_amdgcn_sched_barrier(0);   // issued first: the split below waits only for the older set
     bf16x8 fx[2][3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fx[j][p] = *reinterpret_cast<const bf16x8*>(&Xs[buf][p][64 * wk + 32 * j + c][8 * h]);
+    for (int t = 0; t < 2; ++t) split3_bf16(rx[SET][t], fx[t][0], fx[t][1], fx[t][2]);
+    load(set_c, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bf16x8 fa[3];
@@ -1242,12 +1243,12 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         acc[i][j] = mfma_bf16(fa[0], fx[j][0], t);
       }
     }
-    if (st + 1 < nstages) store(Other{}, buf ^ 1);
+    store_a(Other{}, buf ^ 1);   // (after the last stage: zeros into the idle buffer)
     __syncthreads();
   };
   for (int st = 0; st < nstages; st += 2) {
     iteration(S0{}, st);
-    if (st + 1 < nstages) iteration(S1{}, st + 1);
+    iteration(S1{}, st + 1);
   }
   constexpr int KP = kWT + 1;
   float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
@@ -1262,7 +1263,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         out[(size_t)nn * KP + kk] = acc[i][j][g];
       }
     }
-  // bias column: every staged a value passed through store() exactly once
+  // bias column: every staged a value passed through store_a() exactly once (the rest are zeros)
   bsum[oct][col] = bacc;
   __syncthreads();
   if (tid < kWT) out[(size_t)tid * KP + kWT] = bsum[0][tid] + bsum[1][tid];

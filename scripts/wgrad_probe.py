@@ -14,15 +14,17 @@ M, N, K = 262144, 256, 256
 ITERS = int(os.environ.get("ITERS", "20"))
 lib, dev = L.load(), L.device()
 g = torch.Generator(device=dev).manual_seed(0)
-a = torch.randn(M, L.GRAD_ROW, device=dev, generator=g)
-x = torch.randn(M, L.SAVE_ROW, device=dev, generator=g)
+LDA = int(os.environ.get("LDA", L.GRAD_ROW))   # row strides (floats): the training workspace's by default
+LDX = int(os.environ.get("LDX", L.SAVE_ROW))
+a = torch.randn(M, LDA, device=dev, generator=g)
+x = torch.randn(M, LDX, device=dev, generator=g)
 ow, ob = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
 ws = torch.empty(lib.nerf_wgrad_workspace_bytes(M, N, K), dtype=torch.uint8, device=dev)
 for i in range(ITERS + 2):
     if i == 2:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-    L.check(lib.nerf_wgrad(L.ptr(a), L.GRAD_ROW, N, L.ptr(x), L.SAVE_ROW, K, 1, M, L.ptr(ow), L.ptr(ob), 0, L.ptr(ws),
+    L.check(lib.nerf_wgrad(L.ptr(a), LDA, N, L.ptr(x), LDX, K, 1, M, L.ptr(ow), L.ptr(ob), 0, L.ptr(ws),
                            ws.numel(), L.stream()), "wgrad")
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / ITERS
