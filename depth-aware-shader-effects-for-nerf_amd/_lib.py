@@ -93,12 +93,14 @@ _SIGNATURES = {
     "nerf_depth_normalize": (ctypes.c_int, [_V, _I64, _V, _V, ctypes.c_size_t, _V]),
     "nerf_effect_fog": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V, _V,
                                        ctypes.c_size_t, _V]),
+    "nerf_frame_fog": (ctypes.c_int, [_V, _V, ctypes.c_int, ctypes.c_int, ctypes.c_double, _V, _V, ctypes.c_size_t,
+                                      _V]),
     "nerf_effect_toon": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, _V,
                                         _V, ctypes.c_size_t, _V]),
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 

@@ -99,6 +99,18 @@ __device__ __forceinline__ float cube_rn(float a) {
 //   dn = depth (/ max when max > 1); a = clip(max(dn - start, 0) / (1 - start), 0, 1)**3 * 0.3
 //   out = clip(img * a + 255 * (1 - a), 0, 255) as uint8; without depth: img * 0.05 + 255 * 0.95.
 // start_f / denom_f are float32(fog_start) and float32(1.0 - fog_start) (numpy's weak scalars).
+__device__ __forceinline__ void fog_pixel(const uint8_t (&img)[3], float dn, float dmax, float start_f, float denom_f,
+                                          uint8_t* __restrict__ out) {
+  if (dmax > 1.0f) dn = dn / dmax;
+  float a = fmaxf(dn - start_f, 0.0f) / denom_f;
+  a = fminf(fmaxf(a, 0.0f), 1.0f);
+  a = cube_rn(a);
+  a = a * 0.3f;
+  const float keep = 1.0f - a;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[c] = to_u8((float)img[c] * a + 255.0f * keep);
+}
+
 __global__ void __launch_bounds__(256) fog_kernel(const uint8_t* __restrict__ img, const float* __restrict__ depth,
                                                    int64_t dstride, int64_t P, const unsigned* __restrict__ mm,
                                                    float start_f, float denom_f, uint8_t* __restrict__ out) {
@@ -109,16 +121,26 @@ __global__ void __launch_bounds__(256) fog_kernel(const uint8_t* __restrict__ im
     for (int c = 0; c < 3; ++c) out[3 * p + c] = to_u8((float)img[3 * p + c] * 0.05f + 255.0f * 0.95f);
     return;
   }
-  float dn = depth[p * dstride];
-  const float dmax = ord2f(mm[0]);
-  if (dmax > 1.0f) dn = dn / dmax;
-  float a = fmaxf(dn - start_f, 0.0f) / denom_f;
-  a = fminf(fmaxf(a, 0.0f), 1.0f);
-  a = cube_rn(a);
-  a = a * 0.3f;
-  const float keep = 1.0f - a;
+  const uint8_t px[3] = {img[3 * p], img[3 * p + 1], img[3 * p + 2]};
+  fog_pixel(px, depth[p * dstride], ord2f(mm[0]), start_f, denom_f, out + 3 * p);
+}
+
+// The CLI's Fog frame (run.py:233 -> :248 -> post_processor.py:451-493) from the render outputs in
+// one pass after the depth reduction:
+//   img = uint8(rgb * 255) (truncation), dn = (d - min) / (max - min + 1e-6), Fog(img, dn).
+// Fog's own maximum of dn is the normalised maximum, exactly: the normalisation is two correctly
+// rounded, non-decreasing operations, so max(norm(d)) = norm(max d); no second reduction.
+__global__ void __launch_bounds__(256) frame_fog_kernel(const float* __restrict__ rgb, const float* __restrict__ depth,
+                                                         int64_t P, const unsigned* __restrict__ mm, float start_f,
+                                                         float denom_f, uint8_t* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float mx = ord2f(mm[0]), mn = ord2f(mm[1]);
+  const float range = (mx - mn) + 1e-6f;
+  uint8_t px[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) out[3 * p + c] = to_u8((float)img[3 * p + c] * a + 255.0f * keep);
+  for (int c = 0; c < 3; ++c) px[c] = (uint8_t)(int)(rgb[3 * p + c] * 255.0f);   // rgb in [0, 1]
+  fog_pixel(px, (depth[p] - mn) / range, (mx - mn) / range, start_f, denom_f, out + 3 * p);
 }
 
 // ---------------------------------------------------------------------------------- Toon
@@ -317,6 +339,20 @@ int nerf_effect_fog(const uint8_t* image, const float* depth, int64_t depth_stri
   hipLaunchKernelGGL(fog_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, image, depth, depth_stride, P, mm,
                      (float)fog_start, (float)(1.0 - fog_start), out);
   return check_launch("fog_kernel");
+}
+
+int nerf_frame_fog(const float* rgb, const float* depth, int H, int W, double fog_start, uint8_t* out,
+                   void* workspace, size_t ws_bytes, nerf_stream_t stream) {
+  EREQUIRE(H > 0 && W > 0, "nerf_frame_fog: H=%d W=%d", H, W);
+  EREQUIRE(rgb && depth && out && workspace && ws_bytes >= 256, "nerf_frame_fog: null pointer or workspace < 256 B");
+  EREQUIRE(fog_start < 1.0, "nerf_frame_fog: fog_start=%g must be < 1", fog_start);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t P = (int64_t)H * W;
+  unsigned* mm = (unsigned*)workspace;
+  if (int rc = launch_minmax(depth, P, 1, mm, s)) return rc;
+  hipLaunchKernelGGL(frame_fog_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, rgb, depth, P, mm,
+                     (float)fog_start, (float)(1.0 - fog_start), out);
+  return check_launch("frame_fog_kernel");
 }
 
 int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W, double levels,

@@ -36,6 +36,26 @@ def normalize_depth(depth):
     return out.cpu().numpy() if as_numpy else out
 
 
+def frame_fog(rgb, depth, fog_start=0.1):
+    """The CLI's Fog frame straight from the render outputs (nerf_frame_fog): rgb float (H,W,3) in
+    [0, 1] -> uint8 by truncation (run.py:233), depth float (H,W) normalised (run.py:248), then Fog
+    (post_processor.py:451-493) — one reduction and one per-pixel pass on the GPU instead of a host
+    round trip, a normalisation pass and the effect's own reduction.  Bit-identical to
+    ``PostProcessor`` Fog on ``normalize_depth(depth)`` and ``(rgb * 255).astype(uint8)``.
+    Device tensors in, a uint8 (H,W,3) device tensor out."""
+    lib, dev = _lib.load(), _lib.device()
+    r = torch.as_tensor(rgb).to(dev, torch.float32).contiguous()
+    d = torch.as_tensor(depth).to(dev, torch.float32).contiguous()
+    if r.dim() != 3 or r.shape[2] != 3 or tuple(d.shape) != tuple(r.shape[:2]):
+        raise ValueError(f"frame_fog: rgb {tuple(r.shape)} must be (H,W,3) and depth {tuple(d.shape)} (H,W)")
+    H, W = d.shape
+    out = torch.empty(H, W, 3, dtype=torch.uint8, device=dev)
+    ws = torch.empty(256, dtype=torch.uint8, device=dev)
+    _lib.check(lib.nerf_frame_fog(_lib.ptr(r), _lib.ptr(d), H, W, float(fog_start), _lib.ptr(out), _lib.ptr(ws),
+                                  ws.numel(), _lib.stream()), "nerf_frame_fog")
+    return out
+
+
 class PostProcessor:
     """GPU post-processor with the reference's effect names and parameters."""
 

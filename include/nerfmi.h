@@ -43,7 +43,7 @@ enum nerf_status {
 /* Message of the last failed call on this thread ("" if none). */
 const char* nerf_last_error(void);
 /* ABI version (bumped on any signature or layout change; 7: ReLU mask rows in the training forward
- * and backward, include/nerfmi_train.h). */
+ * and backward, include/nerfmi_train.h; 8: nerf_frame_fog). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays
@@ -187,6 +187,11 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
  * branch).  workspace: nerf_effect_workspace_bytes(H, W) device bytes.
  *   nerf_depth_normalize   run.py:248: (d - min) / (max - min + 1e-6) over n values.
  *   nerf_effect_fog        Fog (post_processor.py:451-493): white fog, fog_start < 1.
+ *   nerf_frame_fog         the CLI's `--shader Fog` frame from the render outputs in one pass after
+ *                          the depth reduction: rgb fp32 (H,W,3) -> uint8 by truncation (run.py:233),
+ *                          depth fp32 (H,W) normalised (run.py:248), then Fog; equal, bit for bit,
+ *                          to nerf_depth_normalize + nerf_effect_fog on the truncated image.
+ *                          workspace >= 256 bytes.
  *   nerf_effect_toon       Toon Shader (post_processor.py:64-117): colours quantised to `levels`
  *                          (> 0; any real value, used as float32 like the reference's numpy scalar),
  *                          depth edges (bilateral 9/75/75, Sobel, threshold 0.05, 3x3 dilation) or,
@@ -198,6 +203,8 @@ int nerf_depth_normalize(const float* depth, int64_t n, float* out, void* worksp
 int nerf_effect_fog(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W,
                     double fog_start, uint8_t* out, void* workspace, size_t ws_bytes,
                     nerf_stream_t stream);
+int nerf_frame_fog(const float* rgb, const float* depth, int H, int W, double fog_start, uint8_t* out,
+                   void* workspace, size_t ws_bytes, nerf_stream_t stream);
 int nerf_effect_toon(const uint8_t* image, const float* depth, int64_t depth_stride, int H, int W,
                      double levels, double edge_strength, uint8_t* out, void* workspace,
                      size_t ws_bytes, nerf_stream_t stream);

@@ -134,7 +134,7 @@ def render_path(model, scene, config, output_dir, num_frames=120, quality='high'
         if world > 1 or not chunk:
             rgb, depth = frames.render_path_frames(model, [c2w], height, width, focal, scene.near, scene.far,
                                                    n_samples, n_imp, seed=seed + frame_idx, **kw)
-            rgb, depth = rgb[0].cpu(), depth[0].cpu()
+            rgb, depth = rgb[0], depth[0]
         else:
             from nerfmi import get_rays
             o, d = get_rays(height, width, focal, c2w.cuda())
@@ -142,8 +142,8 @@ def render_path(model, scene, config, output_dir, num_frames=120, quality='high'
             outs = [render_rays(model, o[j:j + chunk], d[j:j + chunk], scene.near, scene.far, n_samples, n_imp,
                                 seed=(seed + frame_idx) * 1_000_003 + j, **kw)[:2]
                     for j in range(0, o.shape[0], chunk)]
-            rgb = torch.cat([r for r, _ in outs]).reshape(height, width, 3).cpu()
-            depth = torch.cat([dd for _, dd in outs]).reshape(height, width).cpu()
+            rgb = torch.cat([r for r, _ in outs]).reshape(height, width, 3)
+            depth = torch.cat([dd for _, dd in outs]).reshape(height, width)
         if rank != 0:
             continue
         write_frame(output_dir, frame_idx, rgb, depth, save_depth, raw_output, shader)
@@ -152,9 +152,15 @@ def render_path(model, scene, config, output_dir, num_frames=120, quality='high'
 
 
 def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=False, shader=None):
-    """Outputs of run.py:233-275; with `shader`, the effect is applied to the written rgb image
-    (not the raw one) after run.py:248's depth normalisation, both on the GPU."""
+    """Outputs of run.py:233-275 from the frame's device tensors; with `shader`, the effect is
+    applied to the written rgb image (not the raw one) after run.py:248's depth normalisation, both
+    on the GPU (Fog: nerf_frame_fog, straight from the render outputs)."""
     from PIL import Image
+    fogged = None
+    if shader == "Fog" and not raw_output:                    # run.py:233 + :248 + Fog in one GPU pass
+        from nerfmi.post_processor import PostProcessor, frame_fog
+        fogged = frame_fog(rgb, depth, PostProcessor().params["fog_start"]).cpu().numpy()
+    rgb, depth = rgb.cpu(), depth.cpu()
     rgb_img = (rgb * 255).numpy().astype(np.uint8)            # truncation, run.py:233
     depth_img = depth.numpy()
     raw_dir = os.path.join(output_dir, 'raw')
@@ -164,7 +170,9 @@ def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=
         Image.fromarray(rgb_img).save(os.path.join(raw_dir, f'rgb_{frame_idx:03d}.png'))
     if save_depth:
         np.save(os.path.join(raw_dir, f'depth_{frame_idx:03d}.npy'), depth_img)
-    if shader and not raw_output:                             # run.py:247-262
+    if fogged is not None:
+        rgb_img = fogged
+    elif shader and not raw_output:                           # run.py:247-262
         from nerfmi.post_processor import PostProcessor, normalize_depth
         processor = PostProcessor()
         processor.current_effect = shader

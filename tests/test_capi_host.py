@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -61,6 +61,8 @@ def test_bad_arguments_are_reported_not_launched():
     assert lib.nerf_effect_workspace_bytes(800, 800) >= 256 + 2 * 800 * 800 * 4
     rc = lib.nerf_effect_fog(None, None, 1, 8, 8, 0.1, None, None, 0, None)
     assert rc == 1 and b"nerf_effect_fog" in lib.nerf_last_error()
+    assert lib.nerf_frame_fog(None, None, 8, 8, 0.1, None, None, 0, None) == 1
+    assert b"nerf_frame_fog" in lib.nerf_last_error()
     rc = lib.nerf_effect_fog(None, None, 0, 8, 8, 0.1, None, None, 0, None)      # depth stride < 1
     assert rc == 1
     rc = lib.nerf_effect_toon(None, None, 1, 8, 8, 0.0, 1.0, None, None, 0, None)   # levels must be > 0

@@ -113,6 +113,33 @@ def test_fog_matches_oracle(mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("const_depth", [False, True])
+def test_frame_fog_is_the_cli_chain(const_depth):
+    """nerf_frame_fog (run.py:233 truncation -> :248 normalisation -> Fog, one pass after the depth
+    reduction) against the CLI's separate steps on the GPU and against the oracle chain, bit for
+    bit.  rgb covers 0, 1 and every k/255 (the truncation boundaries)."""
+    import nerfmi
+    from nerfmi.post_processor import frame_fog, normalize_depth
+    g = np.random.default_rng(7)
+    H, W = 300, 400
+    rgb = g.random((H, W, 3), dtype=np.float32)
+    rgb.flat[:256] = np.arange(256, dtype=np.float32) / np.float32(255)
+    rgb.flat[256:260] = [0.0, 1.0, np.nextafter(np.float32(1), np.float32(0)), 1e-8]
+    _, depth = scene(seed=9, H=H, W=W)
+    depth = depth + g.normal(0, 0.01, depth.shape).astype(np.float32)
+    if const_depth:
+        depth[:] = 3.25
+    got = frame_fog(torch.from_numpy(rgb).cuda(), torch.from_numpy(depth).cuda()).cpu().numpy()
+    img = (torch.from_numpy(rgb) * 255).numpy().astype(np.uint8)            # run.py:233
+    assert np.array_equal(got, P.fog(img, P.depth_normalize(depth), fog_start=0.1, cube="rn"))
+    pp = nerfmi.PostProcessor()
+    pp.current_effect = "Fog"
+    assert np.array_equal(got, pp.apply_effect(img, normalize_depth(depth)))
+    with pytest.raises(ValueError):
+        frame_fog(torch.from_numpy(rgb).cuda(), torch.from_numpy(depth[:-1]).cuda())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("with_depth,levels", [(True, 5), (False, 5), (True, 4.5), (False, 7.25)])
 def test_toon_matches_oracle(with_depth, levels):
     """Bit for bit, including a non-integer level count (the reference's editor stores
