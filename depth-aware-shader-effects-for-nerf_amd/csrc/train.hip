@@ -1288,7 +1288,7 @@ static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, i
 // order.  A workgroup owns 64 float4 columns of the partial layout; its 4 waves each sum a
 // quarter of the chunks (fixed order), then the quarters are added in order: deterministic.
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w,
+wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w, int ldo,
                     float* __restrict__ out_b, int accumulate) {
   __shared__ f32x4 part[4][64];
   const int KP = K + 1;
@@ -1320,7 +1320,7 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
     const int64_t idx = col4 * 4 + e;
     if (idx >= (int64_t)N * KP) break;
     const int n = (int)(idx / KP), k = (int)(idx % KP);
-    float* dst = k < K ? out_w + (size_t)n * K + k : (out_b ? out_b + n : nullptr);
+    float* dst = k < K ? out_w + (size_t)n * ldo + k : (out_b ? out_b + n : nullptr);
     if (dst) *dst = accumulate ? *dst + sum[e] : sum[e];
   }
 }
@@ -1343,7 +1343,7 @@ static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, 
 }
 
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
-                 float* out_w, float* out_b, int accumulate, float* ws, hipStream_t s) {
+                 float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
@@ -1371,7 +1371,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (rc) return rc;
   const int64_t cols4 = wgrad_stride(N, K) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(256), 0, s, ws, chunks, N, K,
-                     out_w, out_b, accumulate);
+                     out_w, ldo, out_b, accumulate);
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -1565,7 +1565,7 @@ int nerf_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, 
   if (ws_bytes < wgrad_workspace_floats(M, N, K) * 4)
     return set_error(NERF_ERR_WORKSPACE, "nerf_wgrad: workspace %zu < %zu bytes", ws_bytes,
                      wgrad_workspace_floats(M, N, K) * 4);
-  return launch_wgrad(a, lda, N, x, ldx, K, x_div, M, out_w, out_b, accumulate, (float*)workspace,
+  return launch_wgrad(a, lda, N, x, ldx, K, x_div, M, out_w, K, out_b, accumulate, (float*)workspace,
                       (hipStream_t)stream);
 }
 
@@ -1574,31 +1574,40 @@ int nerf_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, 
 static int param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
                        const float* packed, float* const* g, float* dapp, float* ws, size_t ws_floats,
                        hipStream_t s) {
-  struct Job { const float* a; int n; const float* x; int64_t ldx; int K; int64_t xdiv; int p; };
+  // Job: columns [k0, k0 + K) of parameter p's weight gradient (row length ldo) from x; the bias
+  // gradient with the first column block only.  The skip layer's [h3 | enc_x] runs as a 256 x 256
+  // block (the whole-tile kernel) plus the 63 PE columns, instead of one 256 x 319 GEMM on 128 x 128
+  // tiles (416 -> ~300 us per step).
+  struct Job { const float* a; int n; const float* x; int K; int p; int k0; int ldo; bool bias; };
+  constexpr int kSkipK = kHidden + kPosEnc;
   const Job jobs[] = {
-      {grad + 0, kHidden, save + kSaveEncX, kSaveRow, kPosEnc, 1, 0},
-      {grad + 1 * kHidden, kHidden, save + save_h(0), kSaveRow, kHidden, 1, 2},
-      {grad + 2 * kHidden, kHidden, save + save_h(1), kSaveRow, kHidden, 1, 4},
-      {grad + 3 * kHidden, kHidden, save + save_h(2), kSaveRow, kHidden, 1, 6},
-      {grad + 4 * kHidden, kHidden, save + save_h(3), kSaveRow, kHidden + kPosEnc, 1, 8},   // [h3 | enc_x]
-      {grad + 5 * kHidden, kHidden, save + save_h(4), kSaveRow, kHidden, 1, 10},
-      {grad + 6 * kHidden, kHidden, save + save_h(5), kSaveRow, kHidden, 1, 12},
-      {grad + 7 * kHidden, kHidden, save + save_h(6), kSaveRow, kHidden, 1, 14},
-      {grad + kGradSigma, 1, save + save_h(7), kSaveRow, kHidden, 1, P_SIGMA_W},
-      {grad + kGradDir, kDirHidden, save + save_h(7), kSaveRow, kHidden + kDirEnc, 1, P_DIR_W},  // [h7 | enc_d]
-      {grad + kGradRgb, 3, save + kSaveHd, kSaveRow, kDirHidden, 1, P_RGB_W},
+      {grad + 0, kHidden, save + kSaveEncX, kPosEnc, 0, 0, kPosEnc, true},
+      {grad + 1 * kHidden, kHidden, save + save_h(0), kHidden, 2, 0, kHidden, true},
+      {grad + 2 * kHidden, kHidden, save + save_h(1), kHidden, 4, 0, kHidden, true},
+      {grad + 3 * kHidden, kHidden, save + save_h(2), kHidden, 6, 0, kHidden, true},
+      {grad + 4 * kHidden, kHidden, save + save_h(3), kHidden, 8, 0, kSkipK, true},                  // h3 ..
+      {grad + 4 * kHidden, kHidden, save + save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false},  // .. | enc_x
+      {grad + 5 * kHidden, kHidden, save + save_h(4), kHidden, 10, 0, kHidden, true},
+      {grad + 6 * kHidden, kHidden, save + save_h(5), kHidden, 12, 0, kHidden, true},
+      {grad + 7 * kHidden, kHidden, save + save_h(6), kHidden, 14, 0, kHidden, true},
+      {grad + kGradSigma, 1, save + save_h(7), kHidden, P_SIGMA_W, 0, kHidden, true},
+      {grad + kGradDir, kDirHidden, save + save_h(7), kHidden + kDirEnc, P_DIR_W, 0, kHidden + kDirEnc, true},  // [h7 | enc_d]
+      {grad + kGradRgb, 3, save + kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true},
   };
+  static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
   for (const Job& j : jobs) {
     if (wgrad_workspace_floats(M, j.n, j.K) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
-    if ((rc = launch_wgrad(j.a, kGradRow, j.n, j.x, j.ldx, j.K, j.xdiv, M, g[j.p], g[j.p + 1], 0, ws, s))) return rc;
+    if ((rc = launch_wgrad(j.a, kGradRow, j.n, j.x, kSaveRow, j.K, 1, M, g[j.p] + j.k0, j.ldo, j.bias ? g[j.p + 1] : nullptr,
+                           0, ws, s)))
+      return rc;
   }
   if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
     return NERF_OK;
   }
   // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1)
   const int64_t xdiv = app_rows == 1 ? 0 : N;
-  if ((rc = launch_wgrad(grad + kGradHd, kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
+  if ((rc = launch_wgrad(grad + kGradHd, kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W], kAppDim,
                          g[P_APP_B], 0, ws, s)))
     return rc;
   if (!dapp) return NERF_OK;
