@@ -24,6 +24,7 @@ cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) 
 batch on this host's cores.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -79,19 +80,21 @@ def cpu_baseline(target_s):
                       f"train_step on PyTorch-CPU fp32, {t:.1f} s"}
 
 
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary_train.json")
-WGRAD_LAUNCHES = 12   # train.hip param_grads: 11 layer jobs + the appearance projection, each GEMM + reduction
+PMC_SUMMARY = (sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "r*_pmc_summary_train.json"))) or [""])[-1]   # the latest round's
 
 
 def pmc_traffic():
-    """HBM bytes per step of the weight-gradient phase and per data-gradient launch, from the
-    committed PMC passes of `scripts/profile_pmc.sh <dir> train` (2 x FETCH_SIZE + WRITE_SIZE)."""
+    """HBM bytes per step of the weight-gradient phase (every wgrad GEMM and chunk reduction) and
+    per data-gradient launch, from the committed PMC passes of `scripts/profile_pmc.sh <dir> train`
+    (2 x FETCH_SIZE + WRITE_SIZE; scripts/summarize_pmc.py).  Steps in the profiled run = its
+    data-gradient launches (one per step)."""
     try:
         k = json.load(open(PMC_SUMMARY))["kernels"]
-        wgrad = WGRAD_LAUNCHES * (k["nerf::wgrad_bf_kernel"]["hbm_bytes_per_dispatch"]
-                                  + k["nerf::wgrad_reduce_kernel"]["hbm_bytes_per_dispatch"])
+        steps = k["nerf::mlp_backward16_kernel"]["dispatches"]
+        wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items() if "wgrad" in n) / steps
         return {"wgrad": wgrad, "mlp_backward": k["nerf::mlp_backward16_kernel"]["hbm_bytes_per_dispatch"]}
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
         return {}
 
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 measurement refresh on the GPU box: every GPU test, smoke, the render bench with its
 # CPU baseline, rocprofv3 kernel stats of the same bench, the training bench, training PMC
-# traffic passes and training kernel stats.  Each GPU step under its own time limit; the script
+# traffic passes and training kernel stats, render PMC traffic passes.  Each GPU step under its own time limit; the script
 # stops at the first crash / abort / timeout (status >= 124).
 set -o pipefail
 mkdir -p gpurun_out
@@ -22,3 +22,5 @@ step bench_train 600 python bench_train.py --steps 20 --warmup 3
 STEPS=3 WARMUP=1 PASSES="1 2 3" timeout -k 10 600 bash scripts/profile_pmc.sh gpurun_out/pmc_train train; echo "pmc_train rc=$?"
 python scripts/summarize_pmc.py gpurun_out/pmc_train gpurun_out/pmc_train_summary.json; echo "summ rc=$?"
 bash scripts/profile_train.sh > gpurun_out/prof_train_stdout.log 2>&1; echo "prof_train rc=$?"
+STEPS=1 WARMUP=0 PASSES="1 2 3" timeout -k 10 600 bash scripts/profile_pmc.sh gpurun_out/pmc_f16 f16x3; echo "pmc_f16 rc=$?"
+python scripts/summarize_pmc.py gpurun_out/pmc_f16 gpurun_out/pmc_f16_summary.json; echo "summ f16 rc=$?"

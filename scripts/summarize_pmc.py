@@ -25,6 +25,7 @@ for k, cs in per.items():
     kk = res["kernels"][k]
     if "FETCH_SIZE" in kk and "WRITE_SIZE" in kk:   # same gfx950 correction as the MLP figure below
         kk["hbm_bytes_per_dispatch"] = (2 * kk["FETCH_SIZE"] + kk["WRITE_SIZE"]) * 1024
+        kk["dispatches"] = len(cs["FETCH_SIZE"])   # in the profiled run (all shapes of a templated kernel)
 mlp = "nerf::mlp16_kernel" if "nerf::mlp16_kernel" in res["kernels"] else "nerf::mlp_kernel"
 res["mlp_kernel"] = mlp
 m = res["kernels"].get(mlp, {})
