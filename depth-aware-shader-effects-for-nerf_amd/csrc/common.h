@@ -41,6 +41,18 @@ __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { retur
 // inverse CDF, of the fine pass); the device's single-precision expf is a 1-ulp function, torch's
 // CPU exp is correctly rounded on almost every input.  This keeps the reference's fp32
 // expression (one float exp, then the float subtraction) with the best-rounded exp.
+// lo part of the f16 split x = hi + lo: f16(x - hi), through an fma with a -1.0f the compiler
+// cannot fold, so it selects v_fma_mix (f16 hi, f32 x, one f16 rounding) instead of a convert
+// back, a subtract and a convert.  x - hi is exact in f32, so the result is bit-identical.
+__device__ __forceinline__ float opaque_neg_one() {
+  float v = -1.0f;
+  asm("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ _Float16 split_lo(float x, _Float16 hi) {
+  return (_Float16)__builtin_fmaf((float)hi, opaque_neg_one(), x);
+}
+
 __device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
 
 // Counter-based uniform in [0,1) (splitmix64 finaliser), used when the caller

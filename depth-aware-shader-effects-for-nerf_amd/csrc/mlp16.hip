@@ -72,18 +72,11 @@ __device__ __forceinline__ float pow2_scale(float m) {
   return ldexpf(1.0f, 14 - e);
 }
 
-// -1.0f the compiler cannot fold: fma(h, -1, x) stays an fma and selects v_fma_mix (f16 h, f32 x,
-// one f16 rounding) instead of a convert back, a subtract and a convert.  x - h is exact in f32,
-// so the lo part is bit-identical either way; +0.4 % frame rate in a same-box A/B.
-__device__ __forceinline__ float opaque_neg_one() {
-  float v = -1.0f;
-  asm("" : "+s"(v));
-  return v;
-}
+// (split_lo, common.h: +0.4 % frame rate in a same-box A/B against the plain subtract)
 __device__ __forceinline__ void split_into(float x, Operand& op, int j) {
   const _Float16 h = (_Float16)x;
   op.hi[j] = h;
-  op.lo[j] = (_Float16)__builtin_fmaf((float)h, opaque_neg_one(), x);
+  op.lo[j] = split_lo(x, h);
 }
 
 // ---- LDS: one __shared__ array (a second object can make hipcc drain the DMA before every

@@ -493,7 +493,7 @@ __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16
         const float v = X[t][8 * q + j] * sc;
         const _Float16 hi = (_Float16)v;
         bh[2 * t + q][j] = hi;
-        bl[2 * t + q][j] = (_Float16)(v - (float)hi);
+        bl[2 * t + q][j] = split_lo(v, hi);
       }
   return __uint_as_float((uint32_t)(E - 13) << 23);
 }
