@@ -710,7 +710,8 @@ constexpr int kWChunk = 2048;   // samples per chunk
 static inline bool wgrad_whole_tile(int N, int K) { return N == 256 && K == 256; }
 static inline int wgrad_chunk_len(int N, int K) {
   if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
-  if (K <= 64 && N > 64) return kWChunk / 2;
+  if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
+                                                    // 3 % faster but doubled the reduction)
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
   return tiles == 1 ? kWChunk / 4 : tiles == 2 ? kWChunk / 2 : kWChunk;
 }
@@ -1269,6 +1270,119 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   if (tid < kWT) out[(size_t)tid * KP + kWT] = bsum[0][tid] + bsum[1][tid];
 }
 
+// 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
+// columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
+// Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
+// samples 8h .. 8h+7) and splits them in registers; x (64 columns, shared by all waves) is split
+// once per workgroup into LDS (each thread: one column, two samples).  Little LDS and few
+// registers, so two workgroups share a CU and keep more loads in flight (1 KiB of a + 252 B of x
+// per sample).  Loads run two stages ahead, unconditionally.  75 us per 262K-sample launch against
+// 105 us on 256 x 64 tiles of wgrad_bf_kernel (scripts/wgrad_libs_trace.sh, K=63).
+__global__ void __launch_bounds__(512)
+wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int K,
+                    int64_t M, int clen, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][64][kBfRow];
+  const int chunk = blockIdx.x;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  const uint32_t avo = (uint32_t)(8 * h) * lda4 + 4u * (uint32_t)(32 * w + c);
+  // x loader: column tid % 64 (past K: an offset beyond any resource, reads 0), samples 2p, 2p+1
+  const int xc = tid & 63, xp = tid >> 6;
+  const uint32_t xvo = xc < K ? (uint32_t)(2 * xp) * ldx4 + 4u * (uint32_t)xc : 0x80000000u;
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[2][8], rx[2][2];
+  float bacc = 0.0f;
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * lda4), 0));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * ldx4), 0));
+  };
+  auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    __bf16 p[3][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float v = rx[SET][j];
+      const __bf16 h0 = (__bf16)v;
+      const float r1 = v - (float)h0;
+      const __bf16 h1 = (__bf16)r1;
+      p[0][j] = h0;
+      p[1][j] = h1;
+      p[2][j] = (__bf16)(r1 - (float)h1);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<bf16x2*>(&Xs[buf][q][xc][2 * xp]) = bf16x2{p[q][0], p[q][1]};
+    }
+  };
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  const int nstages = (int)((m1 - m0 + 2 * kBfStage - 1) / (2 * kBfStage)) * 2;   // even; the extra reads zeros
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(S0{}, 0);
+  load(S1{}, 1);
+  store_x(S0{}, 0);
+  __syncthreads();
+  // iteration st: split stage st's a (set st % 2) into fragments, reuse the set for stage st+2,
+  // stage st's MFMAs (x from LDS buffer st % 2), stage st+1's x into the other buffer
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    using Other = std::integral_constant<int, 1 - SET>;
+    const int buf = SET;
+    bf16x8 fa[3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bacc += ra[SET][j];
+    split3_bf16(ra[SET], fa[0], fa[1], fa[2]);
+    load(set_c, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 fx[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) fx[q] = *reinterpret_cast<const bf16x8*>(&Xs[buf][q][32 * t + c][8 * h]);
+      f32x16 v = acc[t];
+      v = mfma_bf16(fa[0], fx[2], v);
+      v = mfma_bf16(fa[1], fx[1], v);
+      v = mfma_bf16(fa[2], fx[0], v);
+      v = mfma_bf16(fa[0], fx[1], v);
+      v = mfma_bf16(fa[1], fx[0], v);
+      acc[t] = mfma_bf16(fa[0], fx[0], v);
+    }
+    store_x(Other{}, buf ^ 1);   // (after the last stage: zeros into the idle buffer)
+    __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 2) {
+    iteration(S0{}, st);
+    iteration(S1{}, st + 1);
+  }
+  const int KP = K + 1;
+  float* out = partial + (size_t)chunk * wgrad_stride(kWT, K);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kk = 32 * t + c;
+    if (kk < K) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) out[(size_t)(32 * w + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[t][g];
+    }
+  }
+  // bias column: this lane summed column 32w + c over its 8 samples of every stage
+  bacc += __shfl_xor(bacc, 32);
+  if (h == 0) out[(size_t)(32 * w + c) * KP + K] = bacc;
+}
+
 template <int WN, int WK>
 static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
                            int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
@@ -1356,6 +1470,9 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     if (wgrad_whole_tile(N, K) && x_div == 1) {
       hipLaunchKernelGGL(wgrad_bf256_kernel, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
       rc = check_launch("wgrad_bf256_kernel");
+    } else if (N == kWT && K <= 64 && x_div == 1) {
+      hipLaunchKernelGGL(wgrad_bf_k64_kernel, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M, clen, ws);
+      rc = check_launch("wgrad_bf_k64_kernel");
     } else if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
     else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
   } else if (aligned && K >= 1 && K <= 64 && N > 64)
