@@ -507,20 +507,17 @@ __device__ __forceinline__ void fold_mask(uint32_t (&mask)[4], int c, f32x4 a) {
   for (int e = 0; e < 4; ++e) mask[c / 8] |= (a[e] > 0.0f ? 1u : 0u) << (4 * (c % 8) + e);
 }
 
-// MB: the mask is the forward's 128-bit word for this lane (`mword`, one 16-byte load issued
-// first and waited for only after the MFMA chain), and `act` is unused.
-template <int KS, bool MB>
+// (Without mask rows: nerf_mlp_backward called with masks = NULL.  The training path runs
+// dgrad16_lds below.)
+template <int KS>
 __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const h16x8 (&bh)[16],
                                         const h16x8 (&bl)[16], f32x16 (&out)[8], float inv_w, float inv_g,
-                                        const float* __restrict__ act, const uint32_t* __restrict__ mword,
-                                        uint32_t (&mask)[4], int lane) {
+                                        const float* __restrict__ act, uint32_t (&mask)[4], int lane) {
   constexpr int STEPS = 2 * KS, PIECES = 8 * STEPS, DEPTH = 24;
   constexpr int CPS = 32 / STEPS, LAG = 3, RS = (LAG + 1) * CPS;   // mask chunks per step, load->fold lag
   const u32x4* __restrict__ wf = reinterpret_cast<const u32x4*>(wmat) + lane;
   u32x4 ring[DEPTH];
   f32x4 pf[RS];
-  u32x4 mk;
-  if constexpr (MB) mk = *reinterpret_cast<const u32x4*>(mword);
 #pragma unroll
   for (int i = 0; i < 4; ++i) mask[i] = 0u;
 #pragma unroll
@@ -528,16 +525,14 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
   sfor<STEPS>([&](auto sc) __attribute__((always_inline)) {
     constexpr int st = decltype(sc)::value;
     constexpr int g = st / KS, ks = st % KS;
-    if constexpr (!MB && st >= LAG) {
+    if constexpr (st >= LAG) {
 #pragma unroll
       for (int u = 0; u < CPS; ++u) fold_mask(mask, (st - LAG) * CPS + u, pf[((st - LAG) * CPS + u) % RS]);
     }
-    if constexpr (!MB) {
 #pragma unroll
-      for (int u = 0; u < CPS; ++u) {
-        const int c = st * CPS + u;
-        pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
-      }
+    for (int u = 0; u < CPS; ++u) {
+      const int c = st * CPS + u;
+      pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
     }
     if constexpr (ks == 0) {
 #pragma unroll
@@ -566,13 +561,8 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
     }
     __builtin_amdgcn_sched_barrier(0);
   });
-  if constexpr (MB) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) mask[i] = mk[i];
-  } else {
-#pragma unroll
-    for (int c = (STEPS - LAG) * CPS; c < 32; ++c) fold_mask(mask, c, pf[c % RS]);
-  }
+  for (int c = (STEPS - LAG) * CPS; c < 32; ++c) fold_mask(mask, c, pf[c % RS]);
 }
 
 // relu_back_store with the mask from dgrad16 (tiles 0..NT-1)
@@ -595,13 +585,11 @@ __device__ __forceinline__ void relu_mask_store(f32x16 (&x)[8], const uint32_t (
     }
 }
 
-// MB: ReLU masks from the f16x3 forward's mask rows (one 16-byte slot per layer and lane) instead
-// of the saved f32 activations (1 KiB per layer and sample).
-template <bool MB>
+// Data gradient under f16x3 without mask rows (nerf_mlp_backward with masks = NULL): ReLU masks
+// folded from the saved f32 activations, W^T fragments loaded per wave.
 __global__ void __launch_bounds__(256, 1)
 mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
-                      const float* __restrict__ save, const uint32_t* __restrict__ masks,
-                      const float* __restrict__ sigma, const float* __restrict__ rgb,
+                      const float* __restrict__ save, const float* __restrict__ sigma, const float* __restrict__ rgb,
                       const float* __restrict__ dsigma, const float* __restrict__ drgb, int64_t M,
                       float* __restrict__ grad) {
   const int lane = threadIdx.x & 63;
@@ -646,19 +634,10 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
       }
       grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
     }
-  const uint32_t* mrow = MB ? masks + s * kMaskRow : nullptr;
   uint32_t mask[4];
-  if constexpr (MB) {
-    const uint32_t* md = mrow + (kMaskRDirByte + 8 * h) / 4;
-    mask[0] = md[0];
-    mask[1] = md[1];
-    relu_mask_store<4>(X, mask, gr, kGradDir);
-  } else {
-    relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
-  }
+  relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
   float inv_g = split_rows<4>(X, bh, bl);
-  dgrad16<kDirHidden / 16, MB>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h,
-                               mrow + (kMaskLayerBytes * 7 + 16 * h) / 4, mask, lane);
+  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h, mask, lane);
   const float* wsg = packed + kOffSigmaW;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
@@ -672,9 +651,189 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   for (int l = 7; l >= 1; --l) {
     relu_mask_store(X, mask, gr, l * kHidden);
     inv_g = split_rows<8>(X, bh, bl);
-    dgrad16<kHidden / 16, MB>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h,
-                              mrow + (kMaskLayerBytes * (l - 1) + 16 * h) / 4, mask, lane);
+    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h, mask,
+                          lane);
   }
+  relu_mask_store(X, mask, gr, 0);
+}
+
+// ---- data gradient with an LDS weight stream (f16x3, mask rows: the training path) ------------
+// The 4 waves of a workgroup read the same W^T fragments.  Loading them per wave (dgrad16) costs
+// 256 one-KiB vector loads per wave and layer: more than the texture path moves in the layer's MFMA
+// time.  Here each 16 KiB chunk (2 steps x 4 tiles x {hi, lo} pieces of 1 KiB, the order dgrad16
+// consumes) is DMA'd once per workgroup (global_load_lds_dwordx4, 4 pieces per wave) into a 4-slot
+// LDS ring 3 chunks ahead, published by a vmcnt wait + barrier and read back with ds_read_b128.
+// The stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then
+// trunk layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the
+// kernel reads M0 (as in mlp16.hip's stream).
+constexpr int kBwChunks = 8 + 7 * 16;
+
+struct BwStream {
+  const char* t16;     // packedT
+  const float* ring;   // LDS ring, 4 x 4096 floats
+  uint32_t lds_dma;    // LDS byte address of the ring + 1024 * wave
+  uint32_t voff;       // 16 * lane + 1024 * wave
+};
+
+__device__ __forceinline__ void bw_dma(const BwStream& st, int g) {
+  const size_t layer = g < 8 ? t16_offset(7) : t16_offset(6 - ((g - 8) >> 4));
+  const char* src = st.t16 + layer * 4 + (size_t)(g < 8 ? g : ((g - 8) & 15)) * 16384;
+  const uint32_t dst = st.lds_dma + (uint32_t)(g & 3) * 16384u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    asm volatile(
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %0, %1"
+        :
+        : "v"(st.voff), "s"(src + i * 4096), "s"(dst + i * 4096u)
+        : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void bw_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// dgrad16 with the fragments from the ring and the mask from the forward's mask row (mk: this
+// lane's 128 bits of the layer's output mask): this layer's chunks are g0 .. g0 + KS - 1.
+template <int KS>
+__device__ __forceinline__ void dgrad16_lds(const BwStream& bs, int g0, const h16x8 (&bh)[16], const h16x8 (&bl)[16],
+                                            f32x16 (&out)[8], float inv_w, float inv_g, const u32x4& mk,
+                                            uint32_t (&mask)[4], int lane) {
+  sfor<KS>([&](auto cc) __attribute__((always_inline)) {
+    constexpr int c = decltype(cc)::value;
+    const int g = g0 + c;
+    // own DMA of chunk g done (younger: chunks g+1, g+2 when they exist, and whatever else was
+    // issued after them: counting fewer only waits longer), then the workgroup's
+    if (g + 2 < kBwChunks) bw_wait_vmcnt<8>();
+    else if (g + 1 < kBwChunks) bw_wait_vmcnt<4>();
+    else bw_wait_vmcnt<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 3 < kBwChunks) bw_dma(bs, g + 3);   // into the slot chunk g-1 used (every wave is past it)
+    const float* slot = bs.ring + (g & 3) * 4096;
+    sfor<2>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int st = 2 * c + decltype(sc)::value;
+      constexpr int grp = st / KS, ks = st % KS;
+      u32x4 w[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        w[p] = *reinterpret_cast<const u32x4*>(slot + (8 * decltype(sc)::value + p) * 256 + lane * 4);
+      if constexpr (ks == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[4 * grp + i] = f32x16{};
+      }
+      // small products first: lo(W) hi(g), hi(W) lo(g), then hi(W) hi(g); tiles interleaved
+      sfor<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        out[4 * grp + i] = mfma16t(w[2 * i + 1], bh[ks], out[4 * grp + i]);
+      });
+      sfor<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        out[4 * grp + i] = mfma16t(w[2 * i], bl[ks], out[4 * grp + i]);
+      });
+      sfor<4>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        out[4 * grp + i] = mfma16t(w[2 * i], bh[ks], out[4 * grp + i]);
+      });
+      if constexpr (ks == KS - 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[4 * grp + i] = (out[4 * grp + i] * inv_w) * inv_g;
+      }
+    });
+  });
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mask[i] = mk[i];
+}
+
+// The training path's data gradient (f16x3 with mask rows) with the LDS stream: 1.39 -> 1.33 ms
+// per 262K-sample launch against per-wave fragment loads.  Every wave runs to the end (the stream has
+// barriers and every wave moves a quarter of each chunk): a wave past M works on sample M-1 and
+// stores nothing (its gradient-row resource is empty).
+__global__ void __launch_bounds__(256, 1)
+mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
+                          const uint32_t* __restrict__ masks, const float* __restrict__ sigma,
+                          const float* __restrict__ rgb, const float* __restrict__ dsigma,
+                          const float* __restrict__ drgb, int64_t M, float* __restrict__ grad) {
+  __shared__ __attribute__((aligned(16))) float ring[4 * 4096];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const BwStream bs{reinterpret_cast<const char*>(packedT), ring,
+                    (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)ring + 1024u * wave,
+                    16u * lane + 1024u * wave};
+  bw_dma(bs, 0);
+  bw_dma(bs, 1);
+  bw_dma(bs, 2);
+  const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * 32;   // wave-uniform
+  const int h = lane >> 5;
+  const int64_t s = imin64(s0 + (lane & 31), M - 1);
+  const bool valid = s0 + (lane & 31) < M;
+  float* grow = grad + s * kGradRow;
+  const GradRows gr = grad_rows(grad, s0 < M ? s0 : M, M, lane);
+  const float* invw = packedT + kOffT16Consts + 8;
+
+  // heads, as mlp_backward_kernel
+  float dv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float y = rgb[3 * s + c];
+    dv[c] = drgb[3 * s + c] * (y * (1.0f - y));
+  }
+  const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
+  if (valid && h == 0) {
+    grow[kGradSigma] = dsp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+  }
+  f32x16 X[8];
+  h16x8 bh[16], bl[16];
+  const float* wr = packed + kOffRgbW;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = t * 32 + 8 * q + 4 * h + e;
+        const float d = fmaf(dv[2], wr[2 * kDirHidden + n], fmaf(dv[1], wr[kDirHidden + n], dv[0] * wr[n]));
+        X[t][4 * q + e] = d;
+        v[e] = d;
+      }
+      grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
+    }
+  // the mask words of every layer up front: an ordinary load waited for after DMA pieces were issued
+  // would wait for those too (hipcc does not count the asm), so none is left pending mid-stream
+  const uint32_t* mrow = masks + s * kMaskRow;
+  u32x4 mks[8];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) mks[l] = *reinterpret_cast<const u32x4*>(mrow + (kMaskLayerBytes * l + 16 * h) / 4);
+  uint32_t mask[4];
+  {
+    const uint32_t* md = mrow + (kMaskRDirByte + 8 * h) / 4;
+    mask[0] = md[0];
+    mask[1] = md[1];
+    relu_mask_store<4>(X, mask, gr, kGradDir);
+  }
+  float inv_g = split_rows<4>(X, bh, bl);
+  dgrad16_lds<kDirHidden / 16>(bs, 0, bh, bl, X, invw[7], inv_g, mks[7], mask, lane);
+  const float* wsg = packed + kOffSigmaW;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wsg + t * 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) X[t][4 * q + e] = fmaf(dsp, w[e], X[t][4 * q + e]);
+    }
+  // unrolled: a runtime layer index would select mks[] by GPR indexing, which uses M0
+  sfor<7>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int l = 7 - decltype(ic)::value;
+    relu_mask_store(X, mask, gr, l * kHidden);
+    inv_g = split_rows<8>(X, bh, bl);
+    dgrad16_lds<kHidden / 16>(bs, 8 + (7 - l) * 16, bh, bl, X, invw[l - 1], inv_g, mks[l - 1], mask, lane);
+  });
   relu_mask_store(X, mask, gr, 0);
 }
 
@@ -684,11 +843,11 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3) {
     if (masks)
-      hipLaunchKernelGGL(mlp_backward16_kernel<true>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, save, masks, sigma, rgb, dsigma, drgb, M, grad);
+      hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
+                         packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
     else
-      hipLaunchKernelGGL(mlp_backward16_kernel<false>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, save, masks, sigma, rgb, dsigma, drgb, M, grad);
+      hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
+                         packedT, save, sigma, rgb, dsigma, drgb, M, grad);
     return check_launch("mlp_backward16_kernel");
   }
   hipLaunchKernelGGL(mlp_backward_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed, packedT, save,
