@@ -91,10 +91,10 @@ def pmc_traffic():
     data-gradient launches (one per step)."""
     try:
         k = json.load(open(PMC_SUMMARY))["kernels"]
-        steps = k["nerf::mlp_backward16_kernel"]["dispatches"]
-        wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items() if "wgrad" in n) / steps
-        return {"wgrad": wgrad, "mlp_backward": k["nerf::mlp_backward16_kernel"]["hbm_bytes_per_dispatch"]}
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        bw = next(v for n, v in k.items() if "mlp_backward16" in n)   # (the LDS-stream kernel since r02)
+        wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items() if "wgrad" in n)
+        return {"wgrad": wgrad / bw["dispatches"], "mlp_backward": bw["hbm_bytes_per_dispatch"]}
+    except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
         return {}
 
 
