@@ -128,31 +128,49 @@ __global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restric
 }
 
 // One block per layer: its scale, bound constants (layout.h).
-// Layer statistics for the split scales, one wave per row (lanes over the row's columns, so the
-// loads are coalesced): the row's max |W| and L1 norm, and |bias|, combined over the layer by
-// atomicMax on the float bits (non-negative floats order as unsigned integers: exact in any
-// order).  The raw maxima land in the constants' own slots (zeroed first) and
-// scale16_finalize_kernel turns them into the constants.
+// Layer statistics for the split scales: each wave reduces 8 rows (lanes over the row's columns,
+// so the loads are coalesced) to the rows' max |W|, max L1 norm and max |bias|; the block's 4 waves
+// combine in LDS and one thread per block merges them into the layer's slots by atomicMax on the
+// float bits (non-negative floats order as unsigned integers: exact in any order).  8 blocks per
+// layer: 8 atomics per slot (one atomic per wave and row serialised at L2: 47 us -> a few).  The raw
+// maxima land in the constants' own slots (zeroed first) and scale16_finalize_kernel turns them
+// into the constants.
+constexpr int kS16RowsPerWave = 8;
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
-  const int L = blockIdx.y;
-  const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= layer_rows(L)) return;
-  float mx = 0.0f, l1 = 0.0f;
-  for (int c = lane; c < layer_cols(L); c += 64) {
-    const float w = fabsf(layer_weight(P.p, L, row, c));
-    mx = fmaxf(mx, w);
-    l1 += w;
+  __shared__ float red[3][4];
+  const int L = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float mx = 0.0f, l1m = 0.0f, bm = 0.0f;
+  for (int j = 0; j < kS16RowsPerWave; ++j) {
+    const int row = (blockIdx.x * 4 + wave) * kS16RowsPerWave + j;
+    if (row >= layer_rows(L)) break;
+    float l1 = 0.0f;
+    for (int c = lane; c < layer_cols(L); c += 64) {
+      const float w = fabsf(layer_weight(P.p, L, row, c));
+      mx = fmaxf(mx, w);
+      l1 += w;
+    }
+    for (int off = 32; off > 0; off >>= 1) l1 += __shfl_xor(l1, off);
+    l1m = fmaxf(l1m, l1);
+    if (L < 8) bm = fmaxf(bm, fabsf(P.p[2 * L + 1][row]));
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    mx = fmaxf(mx, __shfl_xor(mx, off));
-    l1 += __shfl_xor(l1, off);
-  }
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   if (lane == 0) {
+    red[0][wave] = mx;
+    red[1][wave] = l1m;
+    red[2][wave] = bm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      mx = fmaxf(mx, red[0][w]);
+      l1m = fmaxf(l1m, red[1][w]);
+      bm = fmaxf(bm, red[2][w]);
+    }
     unsigned* cw = reinterpret_cast<unsigned*>(packed + kOffScale16);
     atomicMax(cw + kS16Sw + L, __float_as_uint(mx));
     if (L < 8) {
-      atomicMax(cw + kS16R + L, __float_as_uint(l1));
-      atomicMax(cw + kS16B + L, __float_as_uint(fabsf(P.p[2 * L + 1][row])));
+      atomicMax(cw + kS16R + L, __float_as_uint(l1m));
+      atomicMax(cw + kS16B + L, __float_as_uint(bm));
     }
   }
 }
@@ -179,7 +197,7 @@ int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   if (int rc = check_launch("pack_kernel")) return rc;
   if (hipMemsetAsync(packed + kOffScale16, 0, kS16Consts * sizeof(float), s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "pack: hipMemsetAsync failed");
-  hipLaunchKernelGGL(scale16_kernel, dim3(kHidden / 4, kS16Layers), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(scale16_kernel, dim3(kHidden / (4 * kS16RowsPerWave), kS16Layers), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("scale16_kernel")) return rc;
   hipLaunchKernelGGL(scale16_finalize_kernel, dim3(1), dim3(64), 0, s, packed);
   if (int rc = check_launch("scale16_finalize_kernel")) return rc;

@@ -61,6 +61,35 @@ def packed_of(state, dev):
     return packed, packedT, ts
 
 
+@pytest.mark.parametrize("scale", [1.0, 37.5])
+def test_device_pack_equals_host_pack(ref_state, scale):
+    """nerf_pack_weights / _transposed on the device (parallel statistics with atomicMax, then the
+    fragment packs) equal the host packers word for word, except the row-L1 bound constants R_L,
+    which the device sums lane-strided and the host sequentially (a few ulp apart; they only bound
+    the activation split scale, a power of two, so the packed fragments are identical)."""
+    L = _lib()
+    lib, dev = L.load(), L.device()
+    st = {k: v * (scale if i % 3 == 0 else 1.0) for i, (k, v) in enumerate(ref_state.items())}
+    ts = [st[k].to(dev).float().contiguous() for k in O.STATE_KEYS]
+    darr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in ts])
+    packed = torch.zeros(lib.nerf_packed_weights_floats(), device=dev)
+    packedT = torch.zeros(lib.nerf_packed_transposed_floats(), device=dev)
+    L.check(lib.nerf_pack_weights(darr, L.ptr(packed), L.stream()), "pack")
+    L.check(lib.nerf_pack_weights_transposed(darr, L.ptr(packedT), L.stream()), "packT")
+    hs = [st[k].float().contiguous() for k in O.STATE_KEYS]
+    arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in hs])
+    hp = np.zeros(lib.nerf_packed_weights_floats(), np.float32)
+    hT = np.zeros(lib.nerf_packed_transposed_floats(), np.float32)
+    assert lib.nerf_pack_weights_host(arr, hp.ctypes.data) == 0
+    assert lib.nerf_pack_weights_transposed_host(arr, hT.ctypes.data) == 0
+    torch.cuda.synchronize()
+    dp = packed.cpu().numpy()
+    diff = np.nonzero(dp.view(np.uint32) != hp.view(np.uint32))[0]
+    assert len(diff) <= 8, diff[:20]                       # at most the 8 trunk layers' R_L
+    assert np.all(np.abs(dp[diff] - hp[diff]) <= 1e-6 * np.abs(hp[diff])), (dp[diff], hp[diff])
+    assert np.array_equal(packedT.cpu().numpy().view(np.uint32), hT.view(np.uint32))
+
+
 # ----------------------------------------------------------------------------- composite backward
 @pytest.mark.parametrize("N", [1, 2, 7, 64, 100, 200])
 def test_composite_backward_matches_autograd(N):
