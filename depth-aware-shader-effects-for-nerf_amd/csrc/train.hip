@@ -659,13 +659,17 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
 
 // ---- data gradient with an LDS weight stream (f16x3, mask rows: the training path) ------------
 // The 4 waves of a workgroup read the same W^T fragments.  Loading them per wave (dgrad16) costs
-// 256 one-KiB vector loads per wave and layer: more than the texture path moves in the layer's MFMA
-// time.  Here each 16 KiB chunk (2 steps x 4 tiles x {hi, lo} pieces of 1 KiB, the order dgrad16
-// consumes) is DMA'd once per workgroup (global_load_lds_dwordx4, 4 pieces per wave) into a 4-slot
-// LDS ring 3 chunks ahead, published by a vmcnt wait + barrier and read back with ds_read_b128.
-// The stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then
-// trunk layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the
-// kernel reads M0 (as in mlp16.hip's stream).
+// 256 one-KiB vector loads per wave and layer.  Here each 16 KiB chunk (2 steps x 4 tiles x
+// {hi, lo} pieces of 1 KiB, the order dgrad16 consumes) is DMA'd once per workgroup
+// (global_load_lds_dwordx4, 4 pieces per wave) into a 4-slot LDS ring, and the fragment reads are
+// software-pipelined as in the forward's stream: a step's MFMAs run while the next step's 8
+// fragments are read, and the barrier that publishes chunk g+1 sits between chunk g's two steps:
+//   [read step 2c+1 (slot g) | MFMA step 2c] wait DMA(g+1), barrier, DMA(g+3) into the slot of
+//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]
+// (every read of chunk g-1 fed an MFMA issued before this barrier, so its slot is free).  The
+// stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then trunk
+// layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the kernel
+// reads M0 (as in mlp16.hip's stream).
 constexpr int kBwChunks = 8 + 7 * 16;
 
 struct BwStream {
@@ -695,54 +699,69 @@ __device__ __forceinline__ void bw_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Publish chunk g (own pieces landed: younger than them are chunk g+1's when it exists, and
+// whatever else was issued after those: counting fewer only waits longer), then start chunk g+2.
+__device__ __forceinline__ void bw_publish(const BwStream& bs, int g) {
+  if (g + 1 < kBwChunks) bw_wait_vmcnt<4>();
+  else bw_wait_vmcnt<0>();
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (g + 2 < kBwChunks) bw_dma(bs, g + 2);
+}
+
+__device__ __forceinline__ void bw_read_step(const BwStream& bs, int g, int half, u32x4 (&w)[8], int lane) {
+  const float* slot = bs.ring + (g & 3) * 4096 + half * 2048;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) w[p] = *reinterpret_cast<const u32x4*>(slot + p * 256 + lane * 4);
+}
+
 // dgrad16 with the fragments from the ring and the mask from the forward's mask row (mk: this
 // lane's 128 bits of the layer's output mask): this layer's chunks are g0 .. g0 + KS - 1.
 template <int KS>
 __device__ __forceinline__ void dgrad16_lds(const BwStream& bs, int g0, const h16x8 (&bh)[16], const h16x8 (&bl)[16],
                                             f32x16 (&out)[8], float inv_w, float inv_g, const u32x4& mk,
                                             uint32_t (&mask)[4], int lane) {
+  u32x4 wa[8], wb[8];
+  bw_publish(bs, g0);
+  bw_read_step(bs, g0, 0, wa, lane);
+  auto step = [&](auto sc, const u32x4 (&w)[8]) __attribute__((always_inline)) {
+    constexpr int st = decltype(sc)::value;
+    constexpr int grp = st / KS, ks = st % KS;
+    if constexpr (ks == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[4 * grp + i] = f32x16{};
+    }
+    // small products first: lo(W) hi(g), hi(W) lo(g), then hi(W) hi(g); tiles interleaved
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * grp + i] = mfma16t(w[2 * i + 1], bh[ks], out[4 * grp + i]);
+    });
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * grp + i] = mfma16t(w[2 * i], bl[ks], out[4 * grp + i]);
+    });
+    sfor<4>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      out[4 * grp + i] = mfma16t(w[2 * i], bh[ks], out[4 * grp + i]);
+    });
+    if constexpr (ks == KS - 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[4 * grp + i] = (out[4 * grp + i] * inv_w) * inv_g;
+    }
+  };
   sfor<KS>([&](auto cc) __attribute__((always_inline)) {
     constexpr int c = decltype(cc)::value;
     const int g = g0 + c;
-    // own DMA of chunk g done (younger: chunks g+1, g+2 when they exist, and whatever else was
-    // issued after them: counting fewer only waits longer), then the workgroup's
-    if (g + 2 < kBwChunks) bw_wait_vmcnt<8>();
-    else if (g + 1 < kBwChunks) bw_wait_vmcnt<4>();
-    else bw_wait_vmcnt<0>();
+    bw_read_step(bs, g, 1, wb, lane);
+    step(std::integral_constant<int, 2 * c>{}, wa);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr (c + 1 < KS) {
+      bw_publish(bs, g + 1);
+      bw_read_step(bs, g + 1, 0, wa, lane);
+    }
+    step(std::integral_constant<int, 2 * c + 1>{}, wb);
     __builtin_amdgcn_sched_barrier(0);
-    if (g + 3 < kBwChunks) bw_dma(bs, g + 3);   // into the slot chunk g-1 used (every wave is past it)
-    const float* slot = bs.ring + (g & 3) * 4096;
-    sfor<2>([&](auto sc) __attribute__((always_inline)) {
-      constexpr int st = 2 * c + decltype(sc)::value;
-      constexpr int grp = st / KS, ks = st % KS;
-      u32x4 w[8];
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-        w[p] = *reinterpret_cast<const u32x4*>(slot + (8 * decltype(sc)::value + p) * 256 + lane * 4);
-      if constexpr (ks == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) out[4 * grp + i] = f32x16{};
-      }
-      // small products first: lo(W) hi(g), hi(W) lo(g), then hi(W) hi(g); tiles interleaved
-      sfor<4>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        out[4 * grp + i] = mfma16t(w[2 * i + 1], bh[ks], out[4 * grp + i]);
-      });
-      sfor<4>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        out[4 * grp + i] = mfma16t(w[2 * i], bl[ks], out[4 * grp + i]);
-      });
-      sfor<4>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        out[4 * grp + i] = mfma16t(w[2 * i], bh[ks], out[4 * grp + i]);
-      });
-      if constexpr (ks == KS - 1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) out[4 * grp + i] = (out[4 * grp + i] * inv_w) * inv_g;
-      }
-    });
   });
 #pragma unroll
   for (int i = 0; i < 4; ++i) mask[i] = mk[i];
@@ -764,7 +783,6 @@ mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restr
                     16u * lane + 1024u * wave};
   bw_dma(bs, 0);
   bw_dma(bs, 1);
-  bw_dma(bs, 2);
   const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * 32;   // wave-uniform
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
