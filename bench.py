@@ -55,6 +55,11 @@ FLOP_PER_SAMPLE = 1_048_832           # SURVEY.md §8d, DESIGN.md §Roofline
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
 MFMA_F16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # f16/bf16 dense MFMA = 16x the f32 rate
 F16X3_ISSUED_FLOP_PER_SAMPLE = 3072 * 32 * 32 * 16 * 2 // 32   # mlp16_kernel MFMAs per 32-sample wave
+# Measured power-limited ceiling of the f16 MFMA stream mlp16 is built from: the
+# trunk half-step alone (12 v_mfma_f32_32x32x16_f16 + 8 LDS fragment reads, no side work, every CU,
+# random operands) holds 1.44 GHz = 1,447 f16 TFLOP/s = 482 TFLOP/s of f16x3 work.
+F16X3_POWER_CEILING = {"value": 1447.0 / 3, "unit": "TFLOP/s",
+                       "source": "profiles/r02_mfma_shape_side.log (scripts/microbench/mfma_shape_side.hip, NV=0)"}
 
 
 def parse():
@@ -184,8 +189,10 @@ def main():
     if rank == 0:
         total_rays = B * len(poses) * args.steps
         traffic, traffic_src = pmc_traffic(args.arith)
+        ceiling = None
         if args.arith == "f16x3":
             kernel, peak = "nerf::mlp16_kernel", MFMA_F16_PEAK_TFLOPS / 3
+            ceiling = dict(F16X3_POWER_CEILING, frac=achieved / F16X3_POWER_CEILING["value"])
             busy = mlp_samples * F16X3_ISSUED_FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS
             dtype = "fp32 (f16x3 split)"
         else:
@@ -216,6 +223,7 @@ def main():
             "mlp_arith": args.arith,
             "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "mfma_busy": busy,
+                         "power_limited_ceiling": ceiling,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "launches": len(launches), "avg_launch_ms": mlp_ms / max(len(launches), 1),
                          "avg_launch_ms_by_pass": {k: sum(v) / len(v) for k, v in per_kind.items()},
