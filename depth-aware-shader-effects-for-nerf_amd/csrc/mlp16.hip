@@ -79,6 +79,21 @@ __device__ __forceinline__ void split_into(float x, Operand& op, int j) {
   op.lo[j] = split_lo(x, h);
 }
 
+// lo parts of a split pair whose hi parts are packed in hi2: f16(x0 - hi.x) | f16(x1 - hi.y), one
+// v_fma_mix each reading its hi half in place (op_sel).  x - hi is exact in f32, so this is
+// bit-identical to split_lo; the compiler, given the same expression, converts both halves back to
+// f32 and packs the residuals with a third convert (or SLP-packs them into v_pk_fma_f32).  Used by
+// the training forward, which is issue-bound (1.28 -> 1.19 ms, same-box A/B); the render kernel
+// measured -0.3 % with it and keeps the compiler's split.
+__device__ __forceinline__ uint32_t split_lo_pair(uint32_t hi2, float x0, float x1) {
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo)
+      : "v"(hi2), "v"(x0), "v"(x1));
+  return lo;
+}
+
 // ---- LDS: one __shared__ array (a second object can make hipcc drain the DMA before every
 // ds_read).  [ring: 4 x 16 KiB][PE: 4 waves x 32 x 64][biases 8 x 256 | density_head w 256, b 4]
 // [layer constants].  Every small vector the layers read sits here: an ordinary global load used
@@ -339,6 +354,7 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
   constexpr int T = T0 + QG / 4, q = QG % 4;
   constexpr int SH = 16 * (T % 2) + 4 * q;
   f32x4 rv;
+  float xs[4];
   uint32_t bits = 0u;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -346,8 +362,24 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     rv[e] = r;
     m = fmaxf(m, r);
     if constexpr (SIGMA) part = fmaf(qv.w[e], r, part);
-    split_into(r * s, in[OP0 + QG / 2], 4 * (q & 1) + e);
+    xs[e] = r * s;
     if constexpr (SV) bits |= (r > 0.0f ? 1u : 0u) << (SH + e);
+    else split_into(xs[e], in[OP0 + QG / 2], 4 * (q & 1) + e);
+  }
+  if constexpr (SV) {   // split: hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
+    Operand& op = in[OP0 + QG / 2];
+    typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const h16x2 hi2 = {(_Float16)xs[2 * p], (_Float16)xs[2 * p + 1]};
+      const h16x2 lo2 =
+          __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), xs[2 * p], xs[2 * p + 1]));
+      const int j = 4 * (q & 1) + 2 * p;
+      op.hi[j] = hi2[0];
+      op.hi[j + 1] = hi2[1];
+      op.lo[j] = lo2[0];
+      op.lo[j + 1] = lo2[1];
+    }
   }
   if constexpr (SV) {
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
