@@ -53,6 +53,21 @@ __device__ __forceinline__ _Float16 split_lo(float x, _Float16 hi) {
   return (_Float16)__builtin_fmaf((float)hi, opaque_neg_one(), x);
 }
 
+// lo parts of a split pair whose hi parts are packed in hi2: f16(x0 - hi.x) | f16(x1 - hi.y), one
+// v_fma_mix each reading its hi half in place (op_sel).  x - hi is exact in f32, so this is
+// bit-identical to split_lo; the compiler, given the same expression, converts both halves back to
+// f32 and packs the residuals with a third convert (or SLP-packs them into v_pk_fma_f32).  Used by
+// the training forward (mlp16.hip, issue-bound: 1.28 -> 1.19 ms, same-box A/B) and the data
+// gradient's row split (train.hip); the render kernel measured -0.3 % with it and keeps its own.
+__device__ __forceinline__ uint32_t split_lo_pair(uint32_t hi2, float x0, float x1) {
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo)
+      : "v"(hi2), "v"(x0), "v"(x1));
+  return lo;
+}
+
 __device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
 
 // Counter-based uniform in [0,1) (splitmix64 finaliser), used when the caller

@@ -79,21 +79,6 @@ __device__ __forceinline__ void split_into(float x, Operand& op, int j) {
   op.lo[j] = split_lo(x, h);
 }
 
-// lo parts of a split pair whose hi parts are packed in hi2: f16(x0 - hi.x) | f16(x1 - hi.y), one
-// v_fma_mix each reading its hi half in place (op_sel).  x - hi is exact in f32, so this is
-// bit-identical to split_lo; the compiler, given the same expression, converts both halves back to
-// f32 and packs the residuals with a third convert (or SLP-packs them into v_pk_fma_f32).  Used by
-// the training forward, which is issue-bound (1.28 -> 1.19 ms, same-box A/B); the render kernel
-// measured -0.3 % with it and keeps the compiler's split.
-__device__ __forceinline__ uint32_t split_lo_pair(uint32_t hi2, float x0, float x1) {
-  uint32_t lo;
-  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-      : "=&v"(lo)
-      : "v"(hi2), "v"(x0), "v"(x1));
-  return lo;
-}
-
 // ---- LDS: one __shared__ array (a second object can make hipcc drain the DMA before every
 // ds_read).  [ring: 4 x 16 KiB][PE: 4 waves x 32 x 64][biases 8 x 256 | density_head w 256, b 4]
 // [layer constants].  Every small vector the layers read sits here: an ordinary global load used

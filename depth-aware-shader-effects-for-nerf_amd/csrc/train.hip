@@ -484,16 +484,20 @@ __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16
   int E = (int)((__float_as_uint(m) >> 23) & 0xffu);
   E = E < 14 ? 14 : E;
   const float sc = __uint_as_float((uint32_t)(267 - E) << 23);
+  typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = X[t][8 * q + j] * sc;
-        const _Float16 hi = (_Float16)v;
-        bh[2 * t + q][j] = hi;
-        bl[2 * t + q][j] = split_lo(v, hi);
+      for (int j = 0; j < 8; j += 2) {   // a pair: hi by one v_cvt_pk_f16_f32, lo by split_lo_pair
+        const float v0 = X[t][8 * q + j] * sc, v1 = X[t][8 * q + j + 1] * sc;
+        const h16x2 hi2 = {(_Float16)v0, (_Float16)v1};
+        const h16x2 lo2 = __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), v0, v1));
+        bh[2 * t + q][j] = hi2[0];
+        bh[2 * t + q][j + 1] = hi2[1];
+        bl[2 * t + q][j] = lo2[0];
+        bl[2 * t + q][j + 1] = lo2[1];
       }
   return __uint_as_float((uint32_t)(E - 13) << 23);
 }
