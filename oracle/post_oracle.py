@@ -5,13 +5,15 @@ The checker for csrc/effects.hip (nerfmi.PostProcessor): a numpy restatement of 
 normalisation of run.py (run.py:248).  Only tests/ import it.
 
 Pinning.  The reference module imports cv2 and tkinter at the top (post_processor.py:2-4), neither
-of which is installed here, so it cannot be imported or run: **parity unpinned** against the
-reference's own outputs.  The Fog effect and the quantisation/combination steps of Toon are
-numpy expressions restated here operation for operation (float32 arrays, Python scalars taken
-as float32 by numpy's weak-scalar rule, astype(uint8) truncating after np.clip).  The cv2 calls of
-Toon (cvtColor RGB2GRAY, bilateralFilter, Sobel, Laplacian, dilate) are restated from OpenCV 4's
-published algorithms (fixed-point gray, bilateralFilter_32f's 4096-bin colour LUT, separable
-Sobel, reflect-101 borders, dilation ignoring the border); cv2 itself is not available to pin them.
+of which is installed here, so it cannot be imported as a whole.  Its Fog method is numpy alone:
+tests/golden/make_post_golden.py compiles that one method from the module's source and records its
+outputs as fixture F9, and `fog(cube="numpy")` equals F9 bit for bit (tests/test_post_effects.py).
+Toon is **parity unpinned**: its quantisation/combination steps are numpy expressions restated
+here operation for operation (float32 arrays, Python scalars taken as float32 by numpy's
+weak-scalar rule, astype(uint8) truncating after np.clip), and its cv2 calls (cvtColor RGB2GRAY,
+bilateralFilter, Sobel, Laplacian, dilate) are restated from OpenCV 4's published algorithms
+(fixed-point gray, bilateralFilter_32f's 4096-bin colour LUT, separable Sobel, reflect-101
+borders, dilation ignoring the border); cv2 itself is not available to pin them.
 """
 import math
 

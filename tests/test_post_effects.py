@@ -1,21 +1,36 @@
 """Depth-aware post effects: nerfmi.PostProcessor's GPU kernels
-(csrc/effects.hip) against oracle/post_oracle.py, and the oracle's own properties on the CPU.
+(csrc/effects.hip) against oracle/post_oracle.py and, for Fog, against the reference's own outputs.
 
-Parity unpinned against the reference itself: src/post_processor.py imports cv2 and tkinter,
-which are absent, so it cannot run here.  The oracle restates Fog and the numpy steps of Toon
-operation for operation and the cv2 steps from OpenCV 4's algorithms (oracle/post_oracle.py).
-Tolerances: none beyond one documented step.  Every operation is an IEEE float32 operation in
-the reference's order on both sides (-ffp-contract=off on the device; the bilateral LUT's exp in
-double, then rounded), so Toon is compared bit for bit, and so is Fog against the oracle with
-the kernel's cube (cube_rn: a**3 rounded once).  The reference's own `adjusted ** 3.0` is
-numpy's float32 SIMD pow, host-dependent and within 1 ulp of cube_rn; against that form a Fog
-value may differ only at a pixel where the two cubes differ (checked pixel by pixel).
+Fog is pinned by fixture F9 (tests/golden/f9_fog.npz, tests/golden/make_post_golden.py): the
+reference's `_effect_fog` (src/post_processor.py:451-493, numpy only) compiled by itself from the
+module's source and run on synthetic frames here, since the module as a whole imports cv2 and
+tkinter, which are absent.  The oracle equals F9 bit for bit; the kernel equals it except where
+the reference's `adjusted ** 3.0` (numpy's float32 SIMD pow, faithfully rounded and
+host-dependent) differs from the correctly rounded cube the kernel computes, and there by at most
+one count.  Toon stays unpinned against the reference: its edge steps are cv2 calls
+(bilateralFilter, Sobel, dilate, cvtColor, Laplacian), restated in the oracle from OpenCV 4's
+algorithms.  Tolerances: none beyond the documented cube step.  Every operation is an IEEE
+float32 operation in the reference's order on both sides (-ffp-contract=off on the device; the
+bilateral LUT's exp in double, then rounded), so Toon is compared bit for bit with the oracle,
+and so is Fog with the oracle's cube_rn form.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from oracle import post_oracle as P
+
+F9 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f9_fog.npz")
+F9_CASES = ["norm", "raw", "chan", "edges", "start0", "start35", "none"]
+
+
+def f9_case(name):
+    z = np.load(F9)
+    depth = z[f"{name}_depth"] if f"{name}_depth" in z else None
+    differs = z[f"{name}_cube_differs"] if depth is not None else None
+    return z[f"{name}_img"], depth, float(z[f"{name}_start"]), z[f"{name}_out"], differs
 
 
 def scene(H=96, W=120, seed=0):
@@ -77,6 +92,48 @@ def test_numpy_cube_is_within_one_ulp_of_cube_rn():
     r = P.cube_rn(a)
     ulps = np.abs(d.view(np.int32).astype(np.int64) - r.view(np.int32))
     assert ulps.max() <= 1
+
+
+@pytest.mark.parametrize("name", F9_CASES)
+def test_oracle_fog_matches_reference_f9(name):
+    """The oracle's Fog is the reference's, bit for bit (F9); with the kernel's rounded cube it
+    differs only where numpy's float32 pow and the rounded cube disagree, by one count at most."""
+    img, depth, start, ref, differs = f9_case(name)
+    rn = P.fog(img, depth, fog_start=start, cube="rn")
+    if depth is None:
+        assert np.array_equal(rn, ref)
+        return
+    dn = np.array(depth if depth.ndim == 2 else depth[..., 0], np.float32)
+    if dn.max() > 1.0:
+        dn = dn / dn.max()
+    a = np.clip(np.maximum(dn - np.float32(start), np.float32(0)) / np.float32(1.0 - start), 0, 1)
+    host_pow_same = np.array_equal(a ** np.float32(3.0) != P.cube_rn(a), differs)
+    if host_pow_same:   # this host's numpy pow rounds as the generating host's did
+        assert np.array_equal(P.fog(img, depth, fog_start=start, cube="numpy"), ref)
+    bad = np.any(rn != ref, axis=2)
+    assert np.all(differs[bad])
+    assert np.abs(rn.astype(int) - ref.astype(int)).max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", F9_CASES)
+def test_fog_matches_reference_f9(name):
+    """The kernel's Fog against the reference's own outputs (F9): equal except where numpy's pow
+    and the rounded cube disagree (stored per pixel in F9), and there within one count; equal to
+    the oracle's rounded-cube form everywhere."""
+    import nerfmi
+    img, depth, start, ref, differs = f9_case(name)
+    pp = nerfmi.PostProcessor()
+    pp.current_effect = "Fog"
+    pp.params["fog_start"] = start
+    got = pp.apply_effect(img, depth)
+    assert np.array_equal(got, P.fog(img, depth, fog_start=start, cube="rn"))
+    bad = np.any(got != ref, axis=2)
+    if depth is None:
+        assert not bad.any()
+    else:
+        assert np.all(differs[bad])
+    assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1
 
 
 @pytest.mark.gpu
