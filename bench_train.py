@@ -182,7 +182,9 @@ def main():
         out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
                "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "scaling": "weak", "vs_baseline": None,
+               "dtype": "fp32 (f16x3 split forward/data gradients, bf16x6 split weight gradients)"
+                        if args.arith == "f16x3" else "fp32",
                "data": "synthetic: teacher-rendered 800x800 scene (SyntheticNeRFDataset, 100 poses), batches "
                        "pre-generated in HBM; student = torch.manual_seed(0); NeRF(Config())",
                "config": {"workload": "chair-style training loop, one image per batch", "rays_per_gpu_per_step":
