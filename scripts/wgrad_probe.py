@@ -10,7 +10,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nerfmi import _lib as L  # noqa: E402
 
-M, N = 262144, 256
+M = 262144
+N = int(os.environ.get("N", "256"))   # 1: density head, 3: rgb head, 128: dir layer
 K = int(os.environ.get("K", "256"))   # 63: layer 0 / the skip layer's PE columns
 ITERS = int(os.environ.get("ITERS", "20"))
 lib, dev = L.load(), L.device()

@@ -262,7 +262,9 @@ def test_wgrad_generic_shapes():
                             (700, 256, 256, 1), (5003, 256, 40, 1), (17, 256, 64, 1),
                             # the production step's shapes: 4096 rays x 64 samples = 262,144 rows
                             (262144, 256, 256, 1), (262144, 256, 63, 1), (262144, 3, 128, 1),
-                            (262144, 128, 32, 64), (262147, 1, 256, 1)]:
+                            (262144, 128, 32, 64), (262147, 1, 256, 1),
+                            # 3 tiles of 128 x 128 (the dir layer): slot-filling chunk length
+                            (262144, 128, 288, 1), (50000, 128, 288, 1)]:
         a = torch.randn(M, N + 3, generator=g)
         xr = 1 if xdiv == 0 else (M + xdiv - 1) // xdiv if xdiv > 1 else M
         x = torch.randn(xr, K + 2, generator=g)
