@@ -278,11 +278,11 @@ def test_wgrad_generic_shapes():
             L.check(lib.nerf_wgrad(L.ptr(ag), N + 3, N, L.ptr(xg), K + 2, K, xdiv, M, L.ptr(ow), L.ptr(ob), acc,
                                    L.ptr(ws), ws.numel(), L.stream()), "wgrad")
         torch.cuda.synchronize()
-        if M < 100000:
+        if M < 10000:
             np.testing.assert_allclose(ow.cpu().numpy(), 2 * exp_w, rtol=1e-4, atol=1e-3)
             np.testing.assert_allclose(ob.cpu().numpy(), 2 * exp_b, rtol=1e-4, atol=1e-3)
         else:
-            # sums of 262K products: an entry near 0 by cancellation has no relative accuracy in any
+            # sums of 50K-262K products: an entry near 0 by cancellation has no relative accuracy in any
             # fp32 order, so each entry's error is measured against its sum of |terms| (the scale of
             # an fp32 summation's error), and the whole against the CPU fp32 GEMM's rel-L2 error
             ad, xd = a[:, :N].abs().double(), x[idx, :K].abs().double()
