@@ -84,7 +84,6 @@ def test_oracle_toon_edges_follow_depth():
     assert np.array_equal(out[~dark], q[~dark])
 
 
-# --------------------------------------------------------------------------------- GPU
 def test_numpy_cube_is_within_one_ulp_of_cube_rn():
     """The one host-dependent step of Fog: numpy's float32 `** 3.0` against cube_rn."""
     a = np.random.default_rng(0).random(1_000_000, dtype=np.float32)
@@ -115,6 +114,7 @@ def test_oracle_fog_matches_reference_f9(name):
     assert np.abs(rn.astype(int) - ref.astype(int)).max() <= 1
 
 
+# --------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", F9_CASES)
 def test_fog_matches_reference_f9(name):
