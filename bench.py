@@ -60,6 +60,10 @@ F16X3_ISSUED_FLOP_PER_SAMPLE = 3072 * 32 * 32 * 16 * 2 // 32   # mlp16_kernel MF
 # random operands) holds 1.44 GHz = 1,447 f16 TFLOP/s = 482 TFLOP/s of f16x3 work.
 F16X3_POWER_CEILING = {"value": 1447.0 / 3, "unit": "TFLOP/s",
                        "source": "profiles/r02_mfma_shape_side.log (scripts/microbench/mfma_shape_side.hip, NV=0)"}
+# The vendor library's sustained f16 GEMM on the same part (torch.matmul -> hipBLASLt, 8192^3, random
+# operands, 3 s back to back): 1,323.5 TFLOP/s = 0.526 of the dense f16 peak.
+VENDOR_F16_GEMM = {"f16_tflops": 1323.5, "frac_of_f16_peak": 1323.5 / MFMA_F16_PEAK_TFLOPS,
+                   "source": "profiles/r02_gemm_f16_ceiling.log (scripts/microbench/gemm_f16_ceiling.py)"}
 
 
 def parse():
@@ -192,8 +196,9 @@ def main():
         ceiling = None
         if args.arith == "f16x3":
             kernel, peak = "nerf::mlp16_kernel", MFMA_F16_PEAK_TFLOPS / 3
-            ceiling = dict(F16X3_POWER_CEILING, frac=achieved / F16X3_POWER_CEILING["value"])
             busy = mlp_samples * F16X3_ISSUED_FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS
+            ceiling = dict(F16X3_POWER_CEILING, frac=achieved / F16X3_POWER_CEILING["value"],
+                           vendor_f16_gemm=dict(VENDOR_F16_GEMM, mlp16_issued_f16_tflops=busy * MFMA_F16_PEAK_TFLOPS))
             dtype = "fp32 (f16x3 split)"
         else:
             kernel, peak = "nerf::mlp_kernel", MFMA_F32_PEAK_TFLOPS
