@@ -175,6 +175,8 @@ def main():
         peaks = {"mlp_forward_train": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
                  "mlp_backward": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
                  "wgrad": MFMA_F32_PEAK_TFLOPS * (16 / 6 if args.arith == "f16x3" else 1)}
+        vendor = ({"mlp_forward_train": 1323.5 / 3, "mlp_backward": 1323.5 / 3, "wgrad": 1377.1 / 6}
+                  if args.arith == "f16x3" else None)
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]
         ach = M * flop / (ms * 1e-3) / 1e12
@@ -198,7 +200,11 @@ def main():
                             "traffic_by_kernel": traffic,
                             "kernels_ms": {k: v[1] for k, v in kern.items()},
                             "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()},
-                            "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()}},
+                            "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()},
+                            # hipBLASLt's own sustained dense GEMM on this part (profiles/r02_gemm_f16_ceiling.log):
+                            # f16 1,323.5 and bf16 1,377.1 TFLOP/s, divided by the split's product count
+                            "kernels_frac_of_vendor_gemm": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / vendor[k]
+                                                            for k, v in kern.items()} if vendor else None},
                "stage_ms": stage_ms, "phase_ms": kt}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
