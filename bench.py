@@ -3,6 +3,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong] [--scene chair|hotdog]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`python bench.py --gpus N` (N > 1, WORLD_SIZE unset) starts the N ranks itself: it runs
+torch.distributed.run as a child process before anything touches the GPU and exits with its status
+(nerfmi/launch.py).  Under a launcher, --gpus must equal WORLD_SIZE (else exit 2).
+--dry-run: the same launcher, process group (gloo, CPU), step plan, all-gather reassembly and
+max-over-ranks timing with a CPU stand-in renderer and 64x64 frames, so the N-rank plumbing is
+tested without a GPU (tests/test_bench_launch.py); its JSON line says "dry_run": true.
+
 One step = get_rays -> render_rays (hierarchical H1: coarse 64, inverse-CDF 128, fine composite
 over the 192 merged samples, the 64 coarse evaluations reused bit-identically so the fine MLP
 evaluates 128) with in-kernel stratified / inverse-CDF RNG, on a random-init NeRF of the
@@ -77,6 +84,7 @@ def parse():
     p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="MLP MFMA arithmetic")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
+    p.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank plumbing (no GPU)")
     return p.parse_args()
 
 
@@ -136,11 +144,71 @@ def workload(scene, world, scaling):
     return [cameras.frame_c2w(scene, "circle", frame=k % 120, num_frames=120) for k in range(n)]
 
 
+def dry_run(args, world, rank):
+    """The N-rank plumbing of a bench step on the CPU: gloo process group, bench.workload's poses,
+    frames.render_frames_sharded's shard plan and all-gather, barrier + max-over-ranks timing; the
+    renderer is a deterministic CPU stand-in (no GPU, no oracle)."""
+    from nerfmi import cameras, frames
+    if world > 1:
+        dist.init_process_group("gloo")
+    Hd = Wd = 64
+    poses = workload(args.scene, world, args.scaling)
+    focal = cameras.synthetic_focal(Wd)
+
+    def ray_fn(frame, row0, nrows):
+        c2w = torch.as_tensor(poses[frame], dtype=torch.float32)
+        i, j = torch.meshgrid(torch.arange(row0, row0 + nrows, dtype=torch.float32),
+                              torch.arange(Wd, dtype=torch.float32), indexing="ij")
+        dirs = torch.stack([(j - Wd * .5) / focal, -(i - Hd * .5) / focal, -torch.ones_like(i)], -1)
+        d = (dirs[..., None, :] * c2w[:3, :3]).sum(-1).reshape(-1, 3)
+        return c2w[:3, 3].expand(d.shape), d
+
+    def render_fn(o, d, offset):
+        idx = torch.arange(offset, offset + o.shape[0], dtype=torch.float64)
+        return torch.sigmoid(o + d).float(), (idx % 997).float()[:, None]
+
+    for _ in range(args.warmup):
+        frames.render_frames_sharded(ray_fn, render_fn, Hd, Wd, len(poses))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rgb, depth = frames.render_frames_sharded(ray_fn, render_fn, Hd, Wd, len(poses))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ranks = [rank]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+        got = [None] * world
+        dist.all_gather_object(got, rank)
+        ranks = got
+    ok = bool(torch.equal(depth.reshape(-1), (torch.arange(depth.numel(), dtype=torch.float64) % 997).float()))
+    if rank == 0:
+        total = Hd * Wd * len(poses) * args.steps
+        print(json.dumps({"metric": "rays/sec (dry run: CPU stand-in renderer, gloo)", "value": total / elapsed,
+                          "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+                          "scaling": args.scaling, "dry_run": True, "ranks": ranks, "reassembly_ok": ok,
+                          "config": {"workload": f"{args.scene} {Hd}x{Wd}, {len(poses)} frame(s) per step",
+                                     "parallelism": f"ray-shard x{world} + all-gather (gloo)"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    from nerfmi import launch
+    rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -157,6 +225,7 @@ def main():
     poses = workload(args.scene, world, args.scaling)
     B = H * W
 
+    @torch.no_grad()
     def step(i):
         rgb, depth = frames.render_path_frames(model, poses, H, W, focal, 2.0, 6.0, N_COARSE, N_FINE,
                                                appearance_embedding=app, perturb=True, hierarchical=True, seed=i)
@@ -238,6 +307,7 @@ def main():
             "psnr_vs_reference_db": None,
         }
         if world == 1 and not args.no_cpu_baseline:
+            @torch.no_grad()
             def gpu_render(o, d, a, t_rand, u_rand):
                 rgb, _, _ = nerfmi.render_rays(model, o.to(dev), d.to(dev), 2.0, 6.0, N_COARSE, N_FINE,
                                                appearance_embedding=a.to(dev), perturb=True, hierarchical=True,

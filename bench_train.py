@@ -3,6 +3,10 @@
     python bench_train.py [--gpus N] [--steps K] [--warmup W] [--batch 4096]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench_train.py --gpus N
 
+`python bench_train.py --gpus N` starts its own N ranks (nerfmi/launch.py, as bench.py); --dry-run
+rehearses the data-parallel plumbing (gloo process group, the flat-gradient all-reduce of
+train.average_gradients, rank-0 broadcast, barrier + max-over-ranks timing) on the CPU.
+
 One step = one iteration of the reference's train_nerf (src/train.py:77-92) per GPU on a
 4096-ray batch of one image, 64 stratified samples per ray (perturb=True; n_importance is
 ignored by the reference's volume_render, render.py:83-86): weight packing, forward with
@@ -52,6 +56,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--arith", default="f16x3", choices=("f16x3", "f32"), help="forward MLP MFMA arithmetic")
+    p.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the N-rank plumbing (no GPU)")
     return p.parse_args()
 
 
@@ -98,11 +103,59 @@ def pmc_traffic():
         return {}
 
 
+def dry_run(args, world, rank):
+    """Data-parallel plumbing of a training step on the CPU: every rank fills the flat gradient
+    buffer (534,276 + 3,200 floats) with its own values, train.average_gradients all-reduces it, and
+    the result must be the mean over ranks; rank 0's parameters are broadcast first."""
+    from nerfmi.train import average_gradients, broadcast_state
+    group = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        group = dist.group.WORLD
+    n = 534_276 + 3_200
+    flat = torch.full((n,), float(rank))
+    broadcast_state([flat], group)
+    ok = bool((flat == 0).all())
+    grad = torch.empty(n)
+    for _ in range(args.warmup):
+        average_gradients(grad.fill_(rank + 1.0), group)
+    if group is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        average_gradients(grad.fill_(rank + 1.0), group)
+    if group is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ok = ok and bool(torch.allclose(grad, torch.full((n,), (world + 1) / 2.0)))
+    ranks = [rank]
+    if group is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank)
+    if rank == 0:
+        print(json.dumps({"metric": "training steps/sec (dry run: gradient all-reduce only, gloo)",
+                          "value": args.steps / elapsed, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+                          "higher_is_better": True, "scaling": "weak", "dry_run": True, "ranks": ranks,
+                          "allreduce_ok": ok, "config": {"parallelism": f"dp{world} (gloo all-reduce)"}}), flush=True)
+    if group is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    from nerfmi import launch
+    rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     torch.cuda.set_device(local)
     group = None
     if world > 1:

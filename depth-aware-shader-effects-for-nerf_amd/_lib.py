@@ -60,7 +60,8 @@ _SIGNATURES = {
     "nerf_render_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                         ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_void_p]),
@@ -73,6 +74,7 @@ _SIGNATURES = {
     "nerf_mlp_forward_train": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V, _V, _V, _V, _V]),
     "nerf_composite_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, ctypes.c_int, ctypes.c_float, _V, _V, _V,
                                                _V]),
+    "nerf_composite_backward_grad": (ctypes.c_int, [_V, _V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V]),
     "nerf_mlp_backward": (ctypes.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, _I64, _V, _V]),
     "nerf_param_grads_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "nerf_param_grads": (ctypes.c_int, [_V, _V, _I64, ctypes.c_int, _V, _I64, _V, ctypes.POINTER(ctypes.c_void_p),
@@ -84,8 +86,8 @@ _SIGNATURES = {
                                  ctypes.c_double, _I64, _V]),
     "nerf_train_workspace_bytes": (ctypes.c_size_t, [_I64, ctypes.c_int]),
     "nerf_train_forward": (ctypes.c_int, [_V, _V, _V, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_int, _V,
-                                          ctypes.c_int, _V, ctypes.c_uint64, _V, _I64, _V, _V, _V, ctypes.c_size_t,
-                                          _V]),
+                                          ctypes.c_int, _V, ctypes.c_uint64, _V, _I64, _V, _V, _V, _V, _V,
+                                          ctypes.c_size_t, _V]),
     "nerf_train_backward": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _I64,
                                            ctypes.POINTER(ctypes.c_void_p), _V, _V, _V, ctypes.c_size_t, _V]),
     # depth-aware post effects (include/nerfmi.h)
@@ -100,7 +102,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 

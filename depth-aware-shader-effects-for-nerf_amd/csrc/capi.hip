@@ -238,7 +238,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 8; }
+int nerf_abi_version(void) { return 9; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -440,10 +440,11 @@ size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf) {
 
 int nerf_render_rays(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
                      double far, int N, int Nf, const float* t_vals, const float* u_lin, int perturb,
-                     const float* t_rand, const float* u_rand, uint64_t seed, const float* app, int64_t app_rows,
-                     float* rgb_map, float* depth_map, float* weights_out, float* z_out, float* coarse_rgb,
-                     float* coarse_depth, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
-  REQUIRE(B >= 0, "nerf_render_rays: B=%lld", (long long)B);
+                     const float* t_rand, const float* u_rand, uint64_t seed, int64_t ray0, const float* app,
+                     int64_t app_rows, float* rgb_map, float* depth_map, float* weights_out, float* z_out,
+                     float* coarse_rgb, float* coarse_depth, void* workspace, size_t ws_bytes,
+                     nerf_stream_t stream) {
+  REQUIRE(B >= 0 && ray0 >= 0, "nerf_render_rays: B=%lld ray0=%lld", (long long)B, (long long)ray0);
   if (N < 1 || N > 4096 || Nf < 0 || N + Nf > 4096 || (Nf > 0 && (N > 256 || Nf > 1024)))
     return set_error(NERF_ERR_UNSUPPORTED, "nerf_render_rays: N=%d Nf=%d outside the supported range", N, Nf);
   if (B == 0) return NERF_OK;
@@ -467,9 +468,12 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   float* wc = (Nf == 0) ? weights_out : region(W_WC);
   float* z_all = z_out ? z_out : region(W_ZALL);
   float* maps = region(W_MAPS);
+  // in-kernel draws keyed by the global ray index ray0 + r (nerf_rng_uniforms)
+  const uint64_t seed_c = rng_key_at(seed, (uint64_t)ray0 * (uint64_t)N);
+  const uint64_t seed_f = rng_key_at(seed ^ 0x5DEECE66Dull, (uint64_t)ray0 * (uint64_t)Nf);
   int rc;
   if ((rc = launch_normalize(rays_d, B, dn, s))) return rc;                                   // render.py:19
-  if ((rc = launch_stratified(rays_o, dn, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed,
+  if ((rc = launch_stratified(rays_o, dn, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed_c,
                               z, nullptr, s)))
     return rc;                                                                                 // render.py:22
   if ((rc = launch_ray_features(packed, dn, B, app, app_rows, feat, s))) return rc;
@@ -486,7 +490,7 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   int* slot = (int*)region(W_SLOT);
   float* rgb_all = region(W_RGBA);
   float* sigma_all = region(W_SIGA);
-  if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed ^ 0x5DEECE66Dull, z_all,
+  if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed_f, z_all,
                               nullptr, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, slot, s)))
     return rc;
   if ((rc = profiled_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_all, sigma_all, slot, T, s))) return rc;

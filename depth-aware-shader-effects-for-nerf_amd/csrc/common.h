@@ -80,6 +80,13 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// The key whose stream starts at index `first` of `seed`'s: hash_uniform(rng_key_at(seed, f), i) ==
+// hash_uniform(seed, f + i) (mod 2^64).  A ray shard keys its draws by the global index of its
+// first ray this way, so a sharded frame draws exactly the uniforms of the unsharded frame.
+__host__ __device__ __forceinline__ uint64_t rng_key_at(uint64_t seed, uint64_t first) {
+  return seed + 0x9E3779B97F4A7C15ull * first;
+}
+
 // Kernel launchers (one per translation unit); each returns a nerf_status.
 int launch_get_rays(int H, int W, float focal, const float* c2w, int row0, int nrows,
                     float* o, float* d, hipStream_t s);

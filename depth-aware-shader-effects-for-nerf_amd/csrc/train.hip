@@ -14,6 +14,8 @@
 //   app_grad_kernel             per-ray appearance-embedding gradient
 //   adam_kernel                 torch.optim.Adam's update, element for element
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <utility>
 
 #include "common.h"
@@ -26,11 +28,16 @@ static_assert(kSaveRow == NERF_SAVE_ROW && kGradRow == NERF_GRAD_ROW, "nerfmi_tr
 // render.py:56-80 differentiated.  With g = d loss / d rgb_map (3), per sample s of a ray:
 //   drgb_s = w_s g;  dw_s = g . rgb_s;  T_s = prod_{j<s} f_j, f_j = 1 - a_j + 1e-10
 //   d a_s = dw_s T_s - (1/f_s) sum_{t>s} dw_t w_t;   d sigma_s = d a_s * dist_s * exp(-sigma_s dist_s)
-// The loss is mean((rgb_map - target)^2) over B x 3 (train.py:87): g = 2 (rgb_map - target)/(3B);
-// sq_err[r] = sum_c (rgb_map - target)^2 for the loss value.
+// The training loss is mean((rgb_map - target)^2) over B x 3 (train.py:87): g = 2 (rgb_map - target)/(3B),
+// sq_err[r] = sum_c (rgb_map - target)^2 for the loss value.  Given an arbitrary upstream gradient
+// instead (autograd: grad_map (B,3) for rgb_map, grad_depth (B) for depth_map, each nullable = 0),
+// g = grad_map[r] and the depth term of depth = S / (A + 1e-10), S = sum w z, A = sum w (:80) adds
+//   dw_s += gd (z_s - S / (A + 1e-10)) / (A + 1e-10)
+// with S and A re-accumulated (double) over the same float weights in the forward pass.
 __global__ void __launch_bounds__(256)
 composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma, const float* __restrict__ zv,
-                          const float* __restrict__ rgb_map, const float* __restrict__ target, int64_t B, int N,
+                          const float* __restrict__ rgb_map, const float* __restrict__ target,
+                          const float* __restrict__ grad_map, const float* __restrict__ grad_depth, int64_t B, int N,
                           float scale, float* __restrict__ dsigma, float* __restrict__ drgb,
                           float* __restrict__ sq_err) {
   const int lane = threadIdx.x & 63;
@@ -40,11 +47,16 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
   float g[3], se = 0.0f;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float e = rgb_map[3 * r + c] - target[3 * r + c];
-    g[c] = scale * e;
-    se += e * e;
+    if (target) {
+      const float e = rgb_map[3 * r + c] - target[3 * r + c];
+      g[c] = scale * e;
+      se += e * e;
+    } else {
+      g[c] = grad_map ? grad_map[3 * r + c] : 0.0f;
+    }
   }
-  if (lane == 0) sq_err[r] = se;
+  const float gd = grad_depth ? grad_depth[r] : 0.0f;
+  if (lane == 0 && sq_err) sq_err[r] = se;
   if (N == 1) {                       // the reference's per-sample tensors are empty (render.py:56-58)
     if (lane == 0) {
       dsigma[base] = 0.0f;
@@ -52,20 +64,22 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
     }
     return;
   }
-  // pass 1 (forward order): transmittance prefix, carried across 64-sample chunks
+  // pass 1 (forward order): transmittance prefix, carried across 64-sample chunks (and, with a
+  // depth gradient, S and A)
   // pass 2 (reverse order): suffix sums of dw*w; done chunk by chunk from the end, recomputing
   // each chunk's T from the stored chunk-start prefixes.
   const int nchunk = (N + 63) / 64;
   __shared__ double carry_lds[4][64]; // T at each chunk start (N <= 4096)
   double* carry_chunk = carry_lds[threadIdx.x >> 6];
-  double carry = 1.0;
+  double carry = 1.0, wz = 0.0, ws = 0.0;
   for (int c = 0; c < nchunk; ++c) {
     const int s = c * 64 + lane;
     double f = 1.0;
+    float alpha = 0.0f, z = 0.0f;
     if (s < N) {
-      const float z = zv[base + s];
+      z = zv[base + s];
       const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
-      const float alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
+      alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
       f = (double)((1.0f - alpha) + 1e-10f);
     }
     double incl = f;
@@ -74,18 +88,36 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
       const double up = __shfl_up(incl, off);
       if (lane >= off) incl *= up;
     }
+    if (gd != 0.0f) {
+      double excl = __shfl_up(incl, 1);
+      if (lane == 0) excl = 1.0;
+      const float w = alpha * (float)(carry * excl);
+      wz += (double)w * (double)z;
+      ws += (double)w;
+    }
     if (lane == 0) carry_chunk[c] = carry;
     carry *= __shfl(incl, 63);
+  }
+  double dinv = 0.0, dmean = 0.0;    // 1 / (A + 1e-10), S / (A + 1e-10)
+  if (gd != 0.0f) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      wz += __shfl_xor(wz, off);
+      ws += __shfl_xor(ws, off);
+    }
+    const double den = (double)((float)ws + 1e-10f);
+    dinv = 1.0 / den;
+    dmean = wz * dinv;
   }
   __builtin_amdgcn_wave_barrier();
   double suffix = 0.0;                // sum_{t > current chunk} dw_t w_t
   for (int c = nchunk - 1; c >= 0; --c) {
     const int s = c * 64 + lane;
     const bool valid = s < N;
-    float alpha = 0.0f, dist = 0.0f, e = 1.0f, fs = 1.0f, sg = 0.0f;
+    float alpha = 0.0f, dist = 0.0f, e = 1.0f, fs = 1.0f, sg = 0.0f, z = 0.0f;
     double f = 1.0;
     if (valid) {
-      const float z = zv[base + s];
+      z = zv[base + s];
       dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
       sg = sigma[base + s];
       e = expf_rn(-sg * dist);
@@ -111,6 +143,7 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
         dw += g[k] * rgb[e3 + k];
         drgb[e3 + k] = w * g[k];
       }
+      if (gd != 0.0f) dw += (float)((double)gd * ((double)z - dmean) * dinv);
     }
     // exclusive suffix sum of dw*w inside the chunk, plus the chunks after it
     double v = valid ? (double)dw * (double)w : 0.0;
@@ -130,11 +163,11 @@ composite_backward_kernel(const float* __restrict__ rgb, const float* __restrict
 }
 
 int launch_composite_backward(const float* rgb, const float* sigma, const float* z, const float* rgb_map,
-                              const float* target, int64_t B, int N, float scale, float* dsigma, float* drgb,
-                              float* sq_err, hipStream_t s) {
+                              const float* target, const float* grad_map, const float* grad_depth, int64_t B, int N,
+                              float scale, float* dsigma, float* drgb, float* sq_err, hipStream_t s) {
   if (B == 0) return NERF_OK;
   hipLaunchKernelGGL(composite_backward_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, rgb, sigma, z,
-                     rgb_map, target, B, N, scale, dsigma, drgb, sq_err);
+                     rgb_map, target, grad_map, grad_depth, B, N, scale, dsigma, drgb, sq_err);
   return check_launch("composite_backward_kernel");
 }
 
@@ -1771,6 +1804,22 @@ static size_t max_wgrad_floats(int64_t M) {
   return m;
 }
 
+// Which MLP arithmetic the last nerf_train_forward on a workspace ran under (the f32 forward writes no
+// mask rows): nerf_train_backward picks the mask source from it, not from the setting in force at
+// backward time.  A small host-side table keyed by workspace address.
+static std::mutex g_ws_mu;
+static std::unordered_map<const void*, int> g_ws_arith;
+static void remember_forward_arith(const void* ws, int arith) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (g_ws_arith.size() > 4096) g_ws_arith.clear();
+  g_ws_arith[ws] = arith;
+}
+static int forward_arith(const void* ws) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  const auto it = g_ws_arith.find(ws);
+  return it == g_ws_arith.end() ? -1 : it->second;
+}
+
 static size_t train_carve(int64_t B, int N, size_t* off) {
   const size_t b = (size_t)B, M = b * (size_t)N;
   const size_t sizes[T_COUNT] = {b * 3, b * N, b * kRayFeat, b * 32, M * 3, M, b * 4, M, M * 3, b,
@@ -1836,8 +1885,18 @@ int nerf_composite_backward(const float* rgb, const float* sigma, const float* z
   if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_composite_backward: N=%d (1..4096)", N);
   TREQUIRE(B == 0 || (rgb && sigma && z_vals && rgb_map && target && dsigma && drgb && sq_err),
            "nerf_composite_backward: null pointer");
-  return launch_composite_backward(rgb, sigma, z_vals, rgb_map, target, B, N, scale, dsigma, drgb, sq_err,
-                                   (hipStream_t)stream);
+  return launch_composite_backward(rgb, sigma, z_vals, rgb_map, target, nullptr, nullptr, B, N, scale, dsigma, drgb,
+                                   sq_err, (hipStream_t)stream);
+}
+
+int nerf_composite_backward_grad(const float* rgb, const float* sigma, const float* z_vals, const float* grad_rgb_map,
+                                 const float* grad_depth_map, int64_t B, int N, float* dsigma, float* drgb,
+                                 nerf_stream_t stream) {
+  TREQUIRE(B >= 0, "nerf_composite_backward_grad: B=%lld", (long long)B);
+  if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_composite_backward_grad: N=%d (1..4096)", N);
+  TREQUIRE(B == 0 || (rgb && sigma && z_vals && dsigma && drgb), "nerf_composite_backward_grad: null pointer");
+  return launch_composite_backward(rgb, sigma, z_vals, nullptr, nullptr, grad_rgb_map, grad_depth_map, B, N, 0.0f,
+                                   dsigma, drgb, nullptr, (hipStream_t)stream);
 }
 
 int nerf_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
@@ -1944,8 +2003,8 @@ size_t nerf_train_workspace_bytes(int64_t B, int N) {
 
 int nerf_train_forward(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
                        double far, int N, const float* t_vals, int perturb, const float* t_rand, uint64_t seed,
-                       const float* app, int64_t app_rows, float* rgb_map, float* depth_map, void* workspace,
-                       size_t ws_bytes, nerf_stream_t stream) {
+                       const float* app, int64_t app_rows, float* rgb_map, float* depth_map, float* weights_out,
+                       float* z_out, void* workspace, size_t ws_bytes, nerf_stream_t stream) {
   TREQUIRE(B >= 0, "nerf_train_forward: B=%lld", (long long)B);
   if (N < 1 || N > 4096) return set_error(NERF_ERR_UNSUPPORTED, "nerf_train_forward: N=%d (1..4096)", N);
   TREQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_train_forward: app_rows=%lld with B=%lld",
@@ -1969,7 +2028,11 @@ int nerf_train_forward(const float* packed, const float* rays_o, const float* ra
   if ((rc = launch_mlp(packed, rays_o, R(T_DIRS), R(T_Z), B, N, R(T_FEAT), R(T_RGB), R(T_SIG), nullptr, 0, s,
                        R(T_SAVE), R(T_ENCD), (uint32_t*)R(T_MASK))))
     return rc;                                                                                          // :49
-  return launch_composite(R(T_RGB), R(T_SIG), R(T_Z), B, N, rgb_map, depth_map, nullptr, s);           // :56-80
+  remember_forward_arith(workspace, g_mlp_arith);
+  if ((rc = launch_composite(R(T_RGB), R(T_SIG), R(T_Z), B, N, rgb_map, depth_map, weights_out, s))) return rc;  // :56-80
+  if (z_out && hipMemcpyAsync(z_out, R(T_Z), (size_t)B * N * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "nerf_train_forward: z copy failed");
+  return NERF_OK;
 }
 
 int nerf_train_backward(const float* packed, const float* packedT, const float* rgb_map, const float* target,
@@ -1988,16 +2051,22 @@ int nerf_train_backward(const float* packed, const float* packedT, const float* 
   char* ws = (char*)workspace;
   auto R = [&](int i) { return (float*)(ws + off[i]); };
   hipStream_t s = (hipStream_t)stream;
+  // the mask rows exist only when this workspace's forward ran under f16x3; the backward's kernels
+  // follow the arithmetic in force now (an f16x3 backward after an f32 forward reads the ReLU masks
+  // from the saved activations instead)
+  const int fwd_arith = forward_arith(workspace);
+  if (fwd_arith < 0)
+    return set_error(NERF_ERR_BAD_ARG, "nerf_train_backward: no nerf_train_forward wrote this workspace");
+  const uint32_t* masks = fwd_arith == NERF_ARITH_F16X3 ? (const uint32_t*)R(T_MASK) : nullptr;
   const int64_t M = B * N;
   int rc;
   const float scale = (float)(2.0 / (3.0 * (double)B));                                              // train.py:87
-  if ((rc = launch_composite_backward(R(T_RGB), R(T_SIG), R(T_Z), rgb_map, target, B, N, scale, R(T_DSIG),
+  if ((rc = launch_composite_backward(R(T_RGB), R(T_SIG), R(T_Z), rgb_map, target, nullptr, nullptr, B, N, scale,
+                                      R(T_DSIG),
                                       R(T_DRGB), R(T_SQE), s)))
     return rc;
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, R(T_SQE), B, loss);
   if ((rc = check_launch("loss_kernel"))) return rc;
-  // the f16x3 forward wrote the mask rows (nerf_train_forward under the same arithmetic)
-  const uint32_t* masks = g_mlp_arith == NERF_ARITH_F16X3 ? (const uint32_t*)R(T_MASK) : nullptr;
   if ((rc = launch_mlp_backward(packed, packedT, R(T_SAVE), masks, R(T_SIG), R(T_RGB), R(T_DSIG), R(T_DRGB), M,
                                 R(T_GRAD), s)))
     return rc;

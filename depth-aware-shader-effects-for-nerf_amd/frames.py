@@ -51,51 +51,72 @@ def shard_rays(ray_fn, H, W, n_frames, start, end):
     return torch.cat(os_), torch.cat(ds_)
 
 
-def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=None):
-    """Render n_frames HxW frames over the ranks of `group`.
-
-    ray_fn(frame, row0, nrows) -> (rays_o, rays_d) for those rows (row-major, (nrows*W, 3));
-    render_fn(rays_o, rays_d, ray_offset) -> (rgb (n,3), depth (n,1)); ray_offset is the global
-    index of the first ray (to key per-ray randomness).
-    Returns (rgb (n_frames,H,W,3), depth (n_frames,H,W)) on every rank.
-    """
-    world, rank = _world(group)
-    total = n_frames * H * W
-    start, end, per = shard_range(total, world, rank)
-    buf = torch.zeros(per, 4, device=device)
+def _render_shard(ray_fn, render_fn, H, W, n_frames, start, end, buf):
     if end > start:
         o, d = shard_rays(ray_fn, H, W, n_frames, start, end)
         rgb, depth = render_fn(o, d, start)
         buf[: end - start, :3] = rgb.to(buf.device)
         buf[: end - start, 3:] = depth.reshape(-1, 1).to(buf.device)
-    if world > 1:
-        out = torch.empty(world * per, 4, device=buf.device)
-        dist.all_gather_into_tensor(out, buf, group=group)
+
+
+def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=None, virtual_shards=None):
+    """Render n_frames HxW frames over the ranks of `group`.
+
+    ray_fn(frame, row0, nrows) -> (rays_o, rays_d) for those rows (row-major, (nrows*W, 3));
+    render_fn(rays_o, rays_d, ray_offset) -> (rgb (n,3), depth (n,1)); ray_offset is the global
+    index of the first ray (it keys per-ray randomness, so the result does not depend on the
+    world size).
+    virtual_shards=G (one process only): render the G shards G ranks would render, one after the
+    other, and reassemble them as the all-gather would (the 1-GPU "G virtual shards"
+    check of the sharding and reassembly of a G-GPU run).
+    Returns (rgb (n_frames,H,W,3), depth (n_frames,H,W)) on every rank.
+    """
+    world, rank = _world(group)
+    total = n_frames * H * W
+    if virtual_shards is not None:
+        if world != 1:
+            raise ValueError("render_frames_sharded: virtual_shards runs in one process (world size 1)")
+        G = int(virtual_shards)
+        per = shard_range(total, G, 0)[2]
+        out = torch.zeros(G * per, 4, device=device)
+        for r in range(G):
+            start, end, _ = shard_range(total, G, r)
+            _render_shard(ray_fn, render_fn, H, W, n_frames, start, end, out[r * per:(r + 1) * per])
     else:
-        out = buf
+        start, end, per = shard_range(total, world, rank)
+        buf = torch.zeros(per, 4, device=device)
+        _render_shard(ray_fn, render_fn, H, W, n_frames, start, end, buf)
+        if world > 1:
+            out = torch.empty(world * per, 4, device=buf.device)
+            dist.all_gather_into_tensor(out, buf, group=group)
+        else:
+            out = buf
     frames = out[:total].reshape(n_frames, H, W, 4)
     return frames[..., :3], frames[..., 3]
 
 
 def render_path_frames(model, poses, H, W, focal, near, far, n_samples, n_importance=0, appearance_embedding=None,
-                       perturb=False, hierarchical=False, seed=0, group=None, timing=None):
+                       perturb=False, hierarchical=False, seed=0, group=None, timing=None, virtual_shards=None):
     """render_frames_sharded with nerfmi's HIP get_rays / render_rays (one list entry per frame:
-    a (3,4)/(4,4) c2w).  timing: passed to render_rays (per-launch MLP events)."""
+    a (3,4)/(4,4) c2w, kept on the host: ray generation takes the pose by value, so no shard
+    synchronises on a device-to-host copy).  The in-kernel draws are keyed by `seed` and the global
+    ray index, so the frames are bit-identical for every world size.  timing: passed to
+    render_rays (per-launch MLP events)."""
     from . import _lib
-    from .ray_utils import get_rays
+    from .ray_utils import rays_on_device
     from .render import render_rays
     dev = _lib.device()
-    c2ws = [torch.as_tensor(p, dtype=torch.float32) for p in poses]
+    c2ws = [torch.as_tensor(p, dtype=torch.float32).detach().cpu() for p in poses]
 
     def ray_fn(frame, row0, nrows):
-        o, d = get_rays(H, W, focal, c2ws[frame].to(dev), rows=(row0, nrows))
-        return o.reshape(-1, 3), d.reshape(-1, 3)
+        return rays_on_device(H, W, focal, c2ws[frame], (row0, nrows), dev)
 
     def render_fn(o, d, offset):
         rgb, depth, _ = render_rays(model, o, d, near, far, n_samples, n_importance,
                                     appearance_embedding=appearance_embedding, perturb=perturb,
-                                    hierarchical=hierarchical, seed=(seed * 1_000_003 + offset) & (2 ** 62 - 1),
+                                    hierarchical=hierarchical, seed=int(seed) & (2 ** 62 - 1), ray_offset=offset,
                                     timing=timing)
         return rgb, depth
 
-    return render_frames_sharded(ray_fn, render_fn, H, W, len(c2ws), group=group, device=dev)
+    return render_frames_sharded(ray_fn, render_fn, H, W, len(c2ws), group=group, device=dev,
+                                 virtual_shards=virtual_shards)

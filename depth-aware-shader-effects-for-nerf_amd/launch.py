@@ -1,0 +1,43 @@
+"""One process per GPU for the benches: `python bench.py --gpus N` starts its own N ranks.
+
+The driver launches the N-GPU bench as `python -m torch.distributed.run --nproc-per-node N ...
+bench.py --gpus N` (WORLD_SIZE set by the launcher); run by hand as `python bench.py --gpus N`, the
+bench starts that same launcher as a child process and exits with its status.  The parent never
+initialises the GPU (no HIP call before the child exists; counting devices does not initialise it
+on this image), so nothing is exec'd from a process that holds the device.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def world_or_launch(gpus, script, argv, check_devices=True):
+    """Return None when this process is a rank that should run (WORLD_SIZE == gpus, or a 1-GPU run),
+    or an exit status: the launched ranks' status, or 2 when --gpus contradicts WORLD_SIZE or the
+    node has fewer GPUs than asked for."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != gpus:
+            sys.stderr.write(f"{os.path.basename(script)}: --gpus {gpus} but WORLD_SIZE={env_world}: "
+                             f"the launcher and the flag must agree\n")
+            return 2
+        return None
+    if gpus <= 1:
+        return None
+    if check_devices:
+        import torch
+        have = torch.cuda.device_count()
+        if have < gpus:
+            sys.stderr.write(f"{os.path.basename(script)}: --gpus {gpus} but {have} GPU(s) visible\n")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", script] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)

@@ -3,10 +3,11 @@
 ``NeRF`` keeps the reference's module tree, parameter names, shapes and
 construction order (src/models.py:58-103), so ``torch.manual_seed(0); NeRF(Config())``
 draws the same weights and ``load_state_dict`` accepts the reference's checkpoints
-(run.py:363).  Its forward runs the fused PE -> MLP HIP kernel (csrc/mlp.hip) on
-weights packed once per parameter version into the MFMA fragment layout
-(csrc/layout.h).  The HIP forward has no autograd (training kernels are a later
-SURVEY.md §8f row): calling it with gradients enabled on trainable parameters raises.
+(run.py:363).  Its forward runs the fused PE -> MLP HIP kernel (csrc/mlp16.hip, csrc/mlp.hip)
+on weights packed once per parameter version into the MFMA fragment layout (csrc/layout.h).
+With gradients enabled and trainable parameters (or an appearance embedding that requires grad)
+the forward runs the training kernels instead and is differentiable (autograd.py): the backward
+is the MFMA data-gradient chain and weight-gradient reductions of csrc/train.hip.
 """
 import ctypes
 
@@ -138,9 +139,9 @@ class NeRF(nn.Module):
     # ------------------------------------------------------------------------ forward
     def forward(self, x, d, appearance_embedding=None):
         """rgb (..., 3), sigma (..., 1) of NeRF.forward (models.py:105-162)."""
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise RuntimeError("nerfmi.NeRF.forward runs the inference HIP kernel (no autograd yet); "
-                               "call it under torch.no_grad()")
+        from . import autograd
+        if autograd.needs_grad(self, appearance_embedding if self.config.use_appearance else None, x, d):
+            return autograd.nerf_forward_grad(self, x, d, appearance_embedding)
         dev = _lib.device()
         lead = x.shape[:-1]
         xs = x.reshape(-1, 3).to(dev, torch.float32).contiguous()

@@ -33,6 +33,16 @@ def draw_seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+_GOLDEN64 = 0x9E3779B97F4A7C15
+_MASK64 = (1 << 64) - 1
+
+
+def rng_key_at(seed, first):
+    """Key of the in-kernel uniform stream shifted to index `first`: u(rng_key_at(s, f), i) ==
+    u(s, f + i) (csrc/common.h rng_key_at; include/nerfmi.h nerf_rng_uniforms)."""
+    return (int(seed) + _GOLDEN64 * int(first)) & _MASK64
+
+
 def get_rays(height, width, focal_length, c2w, *, rows=None):
     """origins (H,W,3) — a 0-stride expand of c2w[:3,3] as in the reference (:48) — and unit
     directions (H,W,3) on c2w's device.  rows=(row0, nrows) generates only those image rows
@@ -48,6 +58,20 @@ def get_rays(height, width, focal_length, c2w, *, rows=None):
                                          _lib.stream()), "nerf_get_rays")
     d = d.to(c2w.device)
     return c2w[..., :3, 3].to(torch.float32).expand(d.shape), d
+
+
+def rays_on_device(height, width, focal_length, c2w_host, rows, dev):
+    """Device (o, d), each (nrows*W, 3), of image rows rows=(row0, nrows) from a host c2w
+    (list/array of 12 floats or a CPU (3,4)/(4,4) tensor): no device-to-host copy of the pose, so a
+    shard loop issues no synchronisation (frames.py)."""
+    m = torch.as_tensor(c2w_host, dtype=torch.float32).reshape(-1, 4)[:3].contiguous()
+    host = (ctypes.c_float * 12)(*m.flatten().tolist())
+    row0, nrows = int(rows[0]), int(rows[1])
+    d = torch.empty(nrows * width, 3, device=dev)
+    _lib.check(_lib.load().nerf_get_rays(height, width, float(focal_length), host, row0, nrows, None, _lib.ptr(d),
+                                         _lib.stream()), "nerf_get_rays")
+    o = m[:, 3].to(dev, non_blocking=True).expand(d.shape)
+    return o, d
 
 
 def sample_stratified(rays_o, rays_d, near, far, n_samples, perturb=True, *, t_rand=None, seed=None):

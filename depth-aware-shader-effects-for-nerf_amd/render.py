@@ -13,6 +13,9 @@ and ``background_color``.  Keyword-only extras:
                       draw (B,Nf) — the reference's torch.rand draws (ray_utils.py:80,119).
   seed                key of the in-kernel RNG when no uniforms are given (drawn from the
                       torch CPU generator by default).
+  ray_offset          global index of the first ray: the in-kernel draws of ray r are those of
+                      ray ray_offset + r of one big batch, so ray shards rendered separately equal
+                      the batch rendered at once, bit for bit (frames.py; include/nerfmi.h).
   timing              optional list; when given, the path runs stage by stage and appends
                       (start, end, samples) per fused-MLP launch, the events recorded around
                       the launch on this stream (bench.py's roofline leg).
@@ -20,14 +23,22 @@ and ``background_color``.  Keyword-only extras:
                       nerf_render_rays call; reuse_coarse=False (staged only) re-evaluates the
                       coarse samples in the fine pass — bit-identical, for the tests.
 ``render_rays`` is the same function (the north-star name).
+
+With gradients enabled and a trainable model (or an appearance embedding that requires grad),
+the reference-compat call (coarse; hierarchical, staged and timing unset) runs the training
+kernels instead (autograd.py): rgb_map and depth_map carry a grad_fn whose backward is the
+composite backward + MLP data-gradient chain + weight-gradient reductions of csrc/train.hip, as
+the reference's training loop needs (src/train.py:77-92).  The H1 hierarchical pass has no
+reference training semantics (render.py:83-86 is a stub) and always renders without a graph.
 """
 import torch
 
 from . import _lib
 from .models import STATE_KEYS, app_rows, pack_params, run_mlp, state_tensors, uses_appearance
-from .ray_utils import draw_seed, linspace_table
+from .ray_utils import draw_seed, linspace_table, rng_key_at
 
 _FOREIGN = {}
+_IMPORTANCE_KEY = 0x5DEECE66D     # the inverse-CDF stream's key: seed ^ this (include/nerfmi.h)
 
 
 def packed_for(model):
@@ -45,7 +56,12 @@ def packed_for(model):
 
 def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, appearance_embedding=None,
                   background_color=None, perturb=True, *, hierarchical=False, t_rand=None, u_rand=None,
-                  seed=None, timing=None, staged=False, reuse_coarse=True):
+                  seed=None, ray_offset=0, timing=None, staged=False, reuse_coarse=True):
+    from . import autograd
+    if not (hierarchical or staged or timing is not None) and \
+            autograd.needs_grad(model, appearance_embedding if uses_appearance(model) else None, rays_o, rays_d):
+        return autograd.volume_render_grad(model, rays_o, rays_d, near, far, n_samples, appearance_embedding,
+                                           perturb, t_rand=t_rand, seed=seed, ray_offset=ray_offset)
     dev = _lib.device()
     lib = _lib.load()
     orig_shape = rays_o.shape
@@ -76,16 +92,17 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
         ws = torch.empty(lib.nerf_render_workspace_bytes(B, N, Nf), dtype=torch.uint8, device=dev)
         _lib.check(lib.nerf_render_rays(
             _lib.ptr(packed), _lib.ptr(o), _lib.ptr(d), B, float(near), float(far), N, Nf, _lib.ptr(t_vals),
-            _lib.ptr(u_lin), int(bool(perturb)), _lib.ptr(tr), _lib.ptr(ur), seed or 0, _lib.ptr(app), rows,
+            _lib.ptr(u_lin), int(bool(perturb)), _lib.ptr(tr), _lib.ptr(ur), seed or 0, int(ray_offset),
+            _lib.ptr(app), rows,
             _lib.ptr(rgb_map), _lib.ptr(depth_map), _lib.ptr(weights), _lib.ptr(z_vals),
             _lib.ptr(crgb) if Nf else None, _lib.ptr(cdepth) if Nf else None, _lib.ptr(ws), ws.numel(),
             _lib.stream()), "nerf_render_rays")
         if Nf:
             cw, cz = None, None
     else:
-        cw, cz = _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed, app, rows,
-                         rgb_map, depth_map, weights, z_vals, crgb if Nf else None, cdepth if Nf else None, timing,
-                         reuse_coarse)
+        cw, cz = _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed or 0,
+                         int(ray_offset), app, rows, rgb_map, depth_map, weights, z_vals, crgb if Nf else None,
+                         cdepth if Nf else None, timing, reuse_coarse)
     out = rays_o.device
     if T == 1:   # the reference's per-sample tensors are empty at one sample (render.py:56-58)
         weights = weights[:, :0]
@@ -100,7 +117,7 @@ def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, app
     return (rgb_map.reshape(*orig_shape[:-1], 3).to(out), depth_map.reshape(*orig_shape[:-1], 1).to(out), extras)
 
 
-def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed, app, rows, rgb_map,
+def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, ur, seed, ray0, app, rows, rgb_map,
             depth_map, weights, z_out, crgb, cdepth, timing, reuse_coarse=True):
     """The kernel sequence of nerf_render_rays, issued stage by stage through the per-stage entry
     points so every fused-MLP launch can be bracketed by events on this stream.  With
@@ -113,7 +130,7 @@ def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, 
     _lib.check(lib.nerf_normalize_dirs(P(d), B, P(dn), s), "nerf_normalize_dirs")
     z = torch.empty(B, N, device=dev)
     _lib.check(lib.nerf_sample_stratified(P(o), P(dn), B, float(near), float(far), N, P(t_vals), int(bool(perturb)),
-                                          P(tr), seed or 0, P(z), None, s), "nerf_sample_stratified")
+                                          P(tr), rng_key_at(seed, ray0 * N), P(z), None, s), "nerf_sample_stratified")
     feat = torch.empty(B, 256, device=dev)
     _lib.check(lib.nerf_ray_features(P(packed), P(dn), B, P(app), rows, P(feat), s), "nerf_ray_features")
     T = N + Nf
@@ -139,7 +156,7 @@ def _staged(lib, packed, o, d, B, near, far, N, Nf, t_vals, u_lin, perturb, tr, 
     _lib.check(lib.nerf_composite(P(rgb_c), P(sigma_c), P(z), B, N, P(crgb), P(cdepth), P(wc), s), "nerf_composite")
     rgb_all = torch.empty(B * T, 3, device=dev)
     sigma_all = torch.empty(B * T, device=dev)
-    key = (seed or 0) ^ 0x5DEECE66D
+    key = rng_key_at(seed ^ _IMPORTANCE_KEY, ray0 * Nf)
     if reuse_coarse:
         z_fine = torch.empty(B, Nf, device=dev)
         slot = torch.empty(B, Nf, dtype=torch.int32, device=dev)

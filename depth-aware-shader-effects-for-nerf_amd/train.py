@@ -42,8 +42,12 @@ class Trainer:
     it before the optimizer step, as DDP would); None trains on this process alone."""
 
     def __init__(self, config, model=None, appearance_embeddings=None, n_images=None, group=None,
-                 lr=None, betas=(0.9, 0.999), eps=1e-8):
+                 lr=None, betas=(0.9, 0.999), eps=1e-8, near=None, far=None):
         self.config = config
+        # the sampling interval: the dataset's near/far (train.py:79 passes dataset.near/far), the
+        # config's when no dataset is given
+        self.near = float(config.near if near is None else near)
+        self.far = float(config.far if far is None else far)
         self.dev = _lib.device()
         self.lib = _lib.load()
         self.group = group
@@ -147,9 +151,9 @@ class Trainer:
             app, rows = self.appearance_embeddings[int(app_idx)].reshape(1, _APP_DIM), 1
         else:
             app, rows = None, 0
-        _lib.check(lib.nerf_train_forward(P(self.packed), P(o), P(d), B, float(self.config.near),
-                                          float(self.config.far), N, P(self._tvals[N]), 1, P(t_rand), int(seed),
-                                          P(app), rows, P(rgb_map), P(depth), P(ws), ws.numel(), s),
+        _lib.check(lib.nerf_train_forward(P(self.packed), P(o), P(d), B, self.near, self.far, N,
+                                          P(self._tvals[N]), 1, P(t_rand), int(seed), P(app), rows, P(rgb_map),
+                                          P(depth), None, None, P(ws), ws.numel(), s),
                    "nerf_train_forward")
         if _marks is not None:
             _marks[1].record(torch.cuda.current_stream())
@@ -201,7 +205,7 @@ class Trainer:
         ck(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), s), "packT")
         ev[1].record(cur)
         ck(lib.nerf_normalize_dirs(P(d), B, P(dn), s), "normalize")
-        ck(lib.nerf_sample_stratified(P(o), P(dn), B, float(self.config.near), float(self.config.far), N,
+        ck(lib.nerf_sample_stratified(P(o), P(dn), B, self.near, self.far, N,
                                       P(self._tvals[N]), 1, None, seed, P(z), None, s), "stratified")
         ck(lib.nerf_ray_features_train(P(self.packed), P(dn), B, P(app), rows, P(feat), P(encd), s), "features")
         ev[2].record(cur)
@@ -330,7 +334,8 @@ def train_nerf(config, dataset, save_dir="checkpoints", group=None, num_iteratio
         os.makedirs(save_dir, exist_ok=True)
     initial_batch_size = min(64, config.batch_size)                    # train.py:26
     trainer = Trainer(config, appearance_embeddings=getattr(dataset, "appearance_embeddings", None),
-                      n_images=len(dataset), group=group)
+                      n_images=len(dataset), group=group, near=getattr(dataset, "near", None),
+                      far=getattr(dataset, "far", None))
     iters = config.num_iterations if num_iterations is None else num_iterations
     losses, psnrs = [], []
     train_nerf.losses, train_nerf.psnrs = losses, psnrs

@@ -43,7 +43,9 @@ enum nerf_status {
 /* Message of the last failed call on this thread ("" if none). */
 const char* nerf_last_error(void);
 /* ABI version (bumped on any signature or layout change; 7: ReLU mask rows in the training forward
- * and backward, include/nerfmi_train.h; 8: nerf_frame_fog). */
+ * and backward, include/nerfmi_train.h; 8: nerf_frame_fog; 9: nerf_render_rays' ray0 (in-kernel
+ * draws keyed by the global ray index), nerf_train_forward's weights/z outputs,
+ * nerf_composite_backward_grad). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays
@@ -64,7 +66,11 @@ int nerf_positional_encoding(const float* x, int64_t M, int dims, int levels, in
 
 /* The in-kernel uniform generator (splitmix64 finaliser of seed + golden*(i+1), top 24 bits):
  * out[i] = u(seed, first + i).  Stratified jitter of sample s of ray r uses u(seed, r*N + s);
- * the inverse-CDF draw j of ray r uses u(seed ^ 0x5DEECE66D, r*Nf + j) inside nerf_render_rays. */
+ * inside nerf_render_rays, whose rays are global rays ray0 .. ray0+B-1, the jitter of sample s of
+ * ray r uses u(seed, (ray0 + r)*N + s) and the inverse-CDF draw j u(seed ^ 0x5DEECE66D,
+ * (ray0 + r)*Nf + j): a frame rendered as ray shards (each with its own ray0) draws exactly the
+ * uniforms of the same frame rendered in one call.  The per-stage entry points take the key of
+ * their first ray, seed + 0x9E3779B97F4A7C15 * first (mod 2^64), the same stream shifted. */
 int nerf_rng_uniforms(uint64_t seed, int64_t first, int64_t n, float* out, nerf_stream_t stream);
 
 /* Per-launch timing of the fused MLP (bench.py's roofline): after nerf_profile_mlp_begin(cap),
@@ -169,13 +175,14 @@ int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, in
  * the reference's compat mode (its n_importance is ignored, render.py:83-86).
  * Outputs: rgb_map (B,3), depth_map (B) of the final pass; weights_out
  * (B,N+Nf or N) and z_out (same) nullable; coarse_rgb/coarse_depth nullable
- * (only written when Nf > 0).  The workspace must hold
+ * (only written when Nf > 0).  ray0: global index of the first ray (keys the in-kernel draws,
+ * nerf_rng_uniforms; 0 for a whole batch).  The workspace must hold
  * nerf_render_workspace_bytes(B, N, Nf) bytes. */
 size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf);
 int nerf_render_rays(const float* packed, const float* rays_o, const float* rays_d, int64_t B,
                      double near, double far, int N, int Nf, const float* t_vals,
                      const float* u_lin, int perturb, const float* t_rand, const float* u_rand,
-                     uint64_t seed, const float* app, int64_t app_rows, float* rgb_map,
+                     uint64_t seed, int64_t ray0, const float* app, int64_t app_rows, float* rgb_map,
                      float* depth_map, float* weights_out, float* z_out, float* coarse_rgb,
                      float* coarse_depth, void* workspace, size_t ws_bytes,
                      nerf_stream_t stream);

@@ -35,16 +35,19 @@ extern "C" {
 /* ---------------------------------------------------------------- whole step
  * Forward of train.py:77-84 (coarse volume_render, n_importance ignored as in
  * render.py:83-86) keeping every activation the backward needs in `workspace`.
- * Arguments as nerf_render_rays with Nf = 0.  B*N < 2^31. */
+ * Arguments as nerf_render_rays with Nf = 0 and ray0 = 0; weights_out (B,N) and z_out (B,N)
+ * are nullable (volume_render's extras).  B*N < 2^31. */
 size_t nerf_train_workspace_bytes(int64_t B, int N);
 int nerf_train_forward(const float* packed, const float* rays_o, const float* rays_d, int64_t B,
                        double near, double far, int N, const float* t_vals, int perturb,
                        const float* t_rand, uint64_t seed, const float* app, int64_t app_rows,
-                       float* rgb_map, float* depth_map, void* workspace, size_t ws_bytes,
-                       nerf_stream_t stream);
+                       float* rgb_map, float* depth_map, float* weights_out, float* z_out,
+                       void* workspace, size_t ws_bytes, nerf_stream_t stream);
 /* loss = mse(rgb_map, target) (train.py:87) into *loss (device float) and its gradient
  * with respect to every parameter (written, not accumulated) and, when dapp is non-null,
- * to the appearance rows (app_rows x 32).  packedT from nerf_pack_weights_transposed. */
+ * to the appearance rows (app_rows x 32).  packedT from nerf_pack_weights_transposed.  The
+ * workspace must hold a nerf_train_forward's saves; the mask source follows the arithmetic that
+ * forward ran under (NERF_ERR_BAD_ARG if no forward wrote it). */
 int nerf_train_backward(const float* packed, const float* packedT, const float* rgb_map,
                         const float* target, int64_t B, int N, const float* app, int64_t app_rows,
                         float* const* param_grads, float* dapp, float* loss, void* workspace,
@@ -71,6 +74,12 @@ int nerf_composite_backward(const float* rgb, const float* sigma, const float* z
                             const float* rgb_map, const float* target, int64_t B, int N,
                             float scale, float* dsigma, float* drgb, float* sq_err,
                             nerf_stream_t stream);
+/* The same for an arbitrary upstream gradient (autograd of volume_render, src/render.py:56-80):
+ * grad_rgb_map (B,3) = d loss / d rgb_map, grad_depth_map (B) = d loss / d depth_map, each
+ * nullable (= 0); dsigma (B,N), drgb (B,N,3) out. */
+int nerf_composite_backward_grad(const float* rgb, const float* sigma, const float* z_vals,
+                                 const float* grad_rgb_map, const float* grad_depth_map, int64_t B,
+                                 int N, float* dsigma, float* drgb, nerf_stream_t stream);
 /* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW).  Under
  * f16x3 the ReLU masks come from `masks` when non-null (an f16x3 forward's), else from the saved
  * activations; the f32 backward always reads the activations. */

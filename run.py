@@ -140,7 +140,7 @@ def render_path(model, scene, config, output_dir, num_frames=120, quality='high'
             o, d = get_rays(height, width, focal, c2w.cuda())
             o, d = o.reshape(-1, 3), d.reshape(-1, 3)
             outs = [render_rays(model, o[j:j + chunk], d[j:j + chunk], scene.near, scene.far, n_samples, n_imp,
-                                seed=(seed + frame_idx) * 1_000_003 + j, **kw)[:2]
+                                seed=seed + frame_idx, ray_offset=j, **kw)[:2]
                     for j in range(0, o.shape[0], chunk)]
             rgb = torch.cat([r for r, _ in outs]).reshape(height, width, 3)
             depth = torch.cat([dd for _, dd in outs]).reshape(height, width)
@@ -189,6 +189,23 @@ def write_frame(output_dir, frame_idx, rgb, depth, save_depth=False, raw_output=
     plt.close()
 
 
+def model_dimension_check(config):
+    """run.py:327-345: the model on 10 random points, without and (with gradients enabled, as the
+    reference calls it) with an appearance embedding."""
+    import torch.nn.functional as F
+    import nerfmi
+    model = nerfmi.NeRF(config).cuda()
+    x = torch.randn(10, 3).cuda()
+    d = F.normalize(torch.randn(10, 3), dim=-1).cuda()
+    with torch.no_grad():
+        rgb, sigma = model(x, d)
+    print(f"Test passed! Output shapes: rgb={tuple(rgb.shape)}, sigma={tuple(sigma.shape)}")
+    if config.use_appearance:
+        rgb, sigma = model(x, d, torch.randn(1, config.appearance_dim).cuda())
+        print(f"Appearance test passed! Output shapes: rgb={tuple(rgb.shape)}, sigma={tuple(sigma.shape)}")
+    return rgb, sigma
+
+
 def main(argv=None):
     args = parse_args(argv)
     import nerfmi
@@ -215,6 +232,7 @@ def main(argv=None):
         from nerfmi.train import train_nerf
         np.random.seed(args.seed + (dist.get_rank() if world > 1 else 0))
         dataset = make_dataset(config)
+        model_dimension_check(config)                                  # run.py:327-345
         torch.manual_seed(args.random_init or 0)
         model = train_nerf(config, dataset, save_dir=args.save_dir, num_iterations=args.iterations,   # run.py:347
                            group=dist.group.WORLD if world > 1 else None)

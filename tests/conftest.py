@@ -80,17 +80,18 @@ def seeded_uniform(seed, shape, sha=None):
     return u
 
 
-def render_h1_f64(state, o, d, app, u, n_samples=64, n_importance=128, chunk=1024):
+def render_h1_f64(state, o, d, app, u, n_samples=64, n_importance=128, chunk=1024, t=None):
     """The oracle's H1 render evaluated in float64 (same expressions and fp32 inputs): the
-    reference truth the fp32 paths are measured against.  CPU tensors; (rgb, depth) float64."""
+    reference truth the fp32 paths are measured against.  CPU tensors; (rgb, depth) float64.
+    t: the stratified jitter uniforms (perturb=True), None for perturb=False."""
     import torch
     from oracle import nerf_oracle as O
     st64 = {k: v.double() for k, v in state.items()}
     outs = []
     for i in range(0, o.shape[0], chunk):
         r, dd, _ = O.render_rays_h1(st64, o[i:i + chunk].double(), d[i:i + chunk].double(), 2.0, 6.0,
-                                    n_samples, n_importance, None if app is None else app.double(), None,
-                                    u[i:i + chunk].double())
+                                    n_samples, n_importance, None if app is None else app.double(),
+                                    None if t is None else t[i:i + chunk].double(), u[i:i + chunk].double())
         outs.append((r, dd))
     return torch.cat([a for a, _ in outs]), torch.cat([b for _, b in outs])
 

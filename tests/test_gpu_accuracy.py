@@ -93,7 +93,7 @@ def model_of(state):
     import nerfmi
     m = nerfmi.NeRF(nerfmi.Config())
     m.load_state_dict(state)
-    return m.cuda().eval()
+    return m.cuda().eval().requires_grad_(False)
 
 
 @pytest.mark.parametrize("which", ["trained", "adversarial"])

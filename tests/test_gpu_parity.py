@@ -48,7 +48,7 @@ def arith(request, nerfmi_mod):
 def model(nerfmi_mod, ref_state):
     m = nerfmi_mod.NeRF(nerfmi_mod.Config())
     m.load_state_dict(ref_state)
-    return m.cuda().eval()
+    return m.cuda().eval().requires_grad_(False)     # the inference kernels (autograd: test_gpu_autograd.py)
 
 
 def crop(golden, scene, n=None):
@@ -149,8 +149,15 @@ def test_forward_ragged_and_position_independent(model, ref_state):
     rgb_o, sigma_o = O.nerf_forward(ref_state, x, d)
     close(rgb, rgb_o, what="rgb")
     close(sigma, sigma_o, what="sigma")
-    with pytest.raises(RuntimeError, match="no_grad"):
-        model(x[:4].cuda(), d[:4].cuda())
+    # with gradients enabled the same call is differentiable (autograd.py, the training kernels)
+    model.requires_grad_(True)
+    try:
+        rgb_g, sigma_g = model(x.cuda(), d.cuda())
+    finally:
+        model.requires_grad_(False)
+    assert rgb_g.grad_fn is not None and sigma_g.grad_fn is not None
+    close(rgb_g, rgb_o, what="rgb (differentiable path)")
+    close(sigma_g, sigma_o, what="sigma (differentiable path)")
 
 
 # ------------------------------------------------------------------------------- composite

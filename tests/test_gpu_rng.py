@@ -39,7 +39,7 @@ def test_render_path_draws_are_the_exposed_generator(ref_state, app_vec):
     from nerfmi import cameras
     m = nerfmi.NeRF(nerfmi.Config())
     m.load_state_dict(ref_state)
-    m = m.cuda().eval()
+    m = m.cuda().eval().requires_grad_(False)
     c2w = cameras.frame_c2w("chair").cuda()
     o, d = nerfmi.get_rays(800, 800, cameras.synthetic_focal(800), c2w)
     o, d = o[380:412, 300:500].reshape(-1, 3), d[380:412, 300:500].reshape(-1, 3)
