@@ -1,0 +1,254 @@
+// The split-f16 MFMA weight stream shared by the fused MLP forward (mlp16.hip) and the data-gradient
+// chain of the training backward (train.hip): the B-operand split, the 4-slot LDS ring that the 4
+// waves of a workgroup fill by LDS-DMA three 16 KiB chunks ahead, and the chunk-step / group
+// drivers that interleave each k-step's MFMAs with the next k-step's fragment reads and with VALU
+// side work (the previous layer's epilogue).  mlp16.hip's header comment describes the schedule.
+#pragma once
+#include "common.h"
+
+namespace nerf {
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kW16Waves = 4;           // waves per workgroup, one per SIMD; they share the weight stream
+
+struct Operand {                       // B operand of one 16-deep k-step, split
+  h16x8 hi, lo;
+};
+
+__device__ __forceinline__ f32x16 mfma16(h16x8 a, h16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// s = 2^(14-e) for a bound m < 2^e (frexp); m = 0 gives e = 0.
+__device__ __forceinline__ float pow2_scale(float m) {
+  int e;
+  frexpf(m, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return ldexpf(1.0f, 14 - e);
+}
+
+// (split_lo, common.h: +0.4 % frame rate in a same-box A/B against the plain subtract)
+__device__ __forceinline__ void split_into(float x, Operand& op, int j) {
+  const _Float16 h = (_Float16)x;
+  op.hi[j] = h;
+  op.lo[j] = split_lo(x, h);
+}
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// ---- the shared weight stream ------------------------------------------------------------
+// Piece I (0..3) of this wave's share of chunk c into LDS slot SLOT: wave w moves pieces w, w+4,
+// w+8, w+12 of the chunk's 16 (1 KiB each).  Inline asm in the saddr form (uniform 64-bit base in
+// SGPRs + the lane's 32-bit offset `voff` = 16*lane + 1024*wave, one VGPR for the whole kernel):
+// the builtin's per-lane 64-bit addresses cost 8 VGPRs per chunk.  hipcc counts none of these
+// loads; the stream waits for them itself (wait_vmcnt).  M0 is declared clobbered rather than
+// saved and restored: -2 SALU per piece, 144K -> 140K cycles per wave, +0.8 % frame rate in a
+// same-box A/B (scripts/ab_bench.sh).  hipcc warns that it does not preserve M0 across such an
+// asm; that is safe only while nothing else in the kernel reads M0 (no LDS-DMA builtin, s_movrel,
+// ds_*_addtid or GWS): the generated code's only M0 writes are these (checked in the .s; the
+// Makefile silences the warning for this file).
+// lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece).
+template <int SLOT, int I>
+__device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
+                                                uint32_t voff) {
+  const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
+#ifdef NERF16_M0_SAVE
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(src + I * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + I * (kW16Waves * 1024))
+      : "memory");
+#else
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, %1"
+      :
+      : "v"(voff), "s"(src + I * (kW16Waves * 1024)), "s"(lds_base + SLOT * (kChunkFloats * 4) + I * (kW16Waves * 1024))
+      : "memory", "m0");
+#endif
+}
+
+// This wave's whole share (4 pieces) of chunk c.
+template <int SLOT>
+__device__ __forceinline__ void chunk_dma(const float* __restrict__ stream, int c, uint32_t lds_base, uint32_t voff) {
+  chunk_dma_piece<SLOT, 0>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 1>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 2>(stream, c, lds_base, voff);
+  chunk_dma_piece<SLOT, 3>(stream, c, lds_base, voff);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
+template <int KK>
+__device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+      a[ti][part] = __builtin_bit_cast(
+          h16x8, *reinterpret_cast<const f32x4*>(slot + ((KK * 4 + ti) * 2 + part) * 256 + lane * 4));
+}
+
+// One k-step of group G (tiles 4G .. 4G+3).
+template <int G, bool FIRST, typename Hook>
+__device__ __forceinline__ void mfma_kstep(const h16x8 (&a)[4][2], const Operand& b, f32x16 (&acc)[8], Hook&& hook) {
+  static_for<4>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    f32x16 c;
+    if constexpr (FIRST) c = mfma16(a[i][1], b.hi, f32x16{});
+    else c = mfma16(a[i][1], b.hi, acc[4 * G + i]);
+    c = mfma16(a[i][0], b.lo, c);
+    acc[4 * G + i] = mfma16(a[i][0], b.hi, c);
+    hook(ic);
+  });
+}
+
+// VALU instructions to place in each MFMA gap of half-step HS of a group whose side work is of
+// kind KIND (see the side lambdas below): one quarter-tile conversion is ~40 VALU instructions,
+// spread over the 12 MFMA gaps of the half-step (an MFMA of 32 cycles hides ~5 single-issue VALU
+// instructions; bunched, they serialise behind it).
+enum SideKind { kSideNone, kSidePrev, kSideCur, kSideL0, kSideSkipPrev, kSideHalf };
+template <int KIND>
+__device__ __forceinline__ constexpr int side_quarters(int hs) {
+  if constexpr (KIND == kSideHalf) return 2;        // 16 quarters over an 8-k-step group (train.hip)
+  if constexpr (KIND == kSidePrev) return hs == 0 ? 2 : (hs <= 14 ? 1 : 0);
+  if constexpr (KIND == kSideSkipPrev) return hs == 0 ? 2 : (hs <= 18 ? 1 : 0);   // + PE operands at 15..18
+  if constexpr (KIND == kSideCur) return hs == 15 ? 2 : (hs >= 1 && hs <= 14 ? 1 : 0);
+  if constexpr (KIND == kSideL0) return 4;
+  return 0;
+}
+// Training forward (SAVE): global stores of ReLU(y) (one f32x4 per converted quarter) issued in
+// half-step hs; they count in vmcnt with the stream's DMA (skip-layer PE operands store nothing).
+template <int KIND>
+__device__ __forceinline__ constexpr int side_stores(int hs) {
+  if constexpr (KIND == kSideSkipPrev) return side_quarters<kSidePrev>(hs);
+  return side_quarters<KIND>(hs);
+}
+template <int KIND>
+__device__ __forceinline__ constexpr int side_vpg(int hs) {
+  const int q = side_quarters<KIND>(hs);
+#ifndef NERF16_VALU_PER_QUARTER
+#define NERF16_VALU_PER_QUARTER 40
+#endif
+  return q == 0 ? 0 : (q * NERF16_VALU_PER_QUARTER + 10) / 11;
+}
+
+// Half a chunk-step: one k-step's MFMAs (fragments `am`) with the next k-step's fragment reads
+// (into `ar`, from `slot_r`) and the side work (VALU) interleaved: per MFMA gap one ds_read_b128
+// (8 of the 12 gaps) and VPG VALU instructions.
+template <int G, bool FIRST, bool READ, int KK_R, int VPG, typename Side, typename Hook>
+__device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand& b, f32x16 (&acc)[8],
+                                          const float* slot_r, h16x8 (&ar)[4][2], int lane, Side&& side,
+                                          Hook&& hook) {
+  // the side work's small LDS reads (bias, density weights) go first: LDS returns in order, so its
+  // VALU then waits for them alone, not for the fragment reads issued after them
+  side(std::integral_constant<int, 0>{});
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
+  mfma_kstep<G, FIRST>(am, b, acc, hook);
+  side(std::integral_constant<int, 1>{});
+#ifndef NERF16_DSR_PER_GAP
+#define NERF16_DSR_PER_GAP 1
+#endif
+#ifndef NERF16_DSR_GAP0
+#define NERF16_DSR_GAP0 2
+#endif
+#ifndef NERF16_VALU_GAP0
+#define NERF16_VALU_GAP0 1
+#endif
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // 1 MFMA
+    if constexpr (READ) {
+      if (i >= NERF16_DSR_GAP0 && i < NERF16_DSR_GAP0 + 8 / NERF16_DSR_PER_GAP)
+        __builtin_amdgcn_sched_group_barrier(0x100, NERF16_DSR_PER_GAP, 0);   // DS reads
+    }
+    if constexpr (VPG > 0) {
+      if (i >= NERF16_VALU_GAP0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VPG VALU (none in
+    }                                                                                   // gap 0: bias reads land)
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Chunk-step: k-steps 2i, 2i+1 of group G from the chunk in LDS slot SLOT (global chunk c);
+// FIRST (the group's first chunk) starts the accumulators from 0 at k-step 0.
+//   MFMA k-step 0, reading k-step 1's A | wait own DMA of chunk c+1, barrier | DMA chunk c+3 into
+//   the slot chunk c-1 used | MFMA k-step 1, reading chunk c+1's k-step-0 A
+// On entry chunk c is published, c+1 and c+2 are in flight and a0 holds k-step 0's fragments.
+// TAIL = chunks left after c, capped at 3: the stream's last steps stop loading and waiting.
+template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, bool SV, typename Side0, typename Side1>
+__device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int c, float* lds, uint32_t lds_dma,
+                                           uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
+                                           const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
+                                           Side1&& side1) {
+  // (the fragment reads' lgkmcnt waits are the compiler's, per MFMA)
+  half_step<G, FIRST, true, 1, side_vpg<KIND>(HS0)>(a0, b0, acc, lds + SLOT * kChunkFloats, a1, lane, side0,
+                                                    [](auto) {});
+  // own DMA of chunk c+1 done.  Younger than its pieces (issued in chunk-step c-2's second half)
+  // are chunk c+2's 4 pieces and, with stores in the side work (SV), at least the stores of this
+  // half-step and of chunk-step c-1's two half-steps: counting them leaves those stores in flight
+  // (vmcnt retires in issue order, so a smaller count would also wait for stores issued after the
+  // pieces; counting fewer than are younger only waits longer).  In a group's first chunk-step the
+  // previous half-steps belong to another side schedule and are not counted.
+#ifdef NERF16_WAIT_STORES_STRICT   // A/B: count this half-step's stores only
+  constexpr int kPrevStores = 0;
+#else
+  constexpr int kPrevStores = (SV && !FIRST) ? side_stores<KIND>(HS0 - 1) + side_stores<KIND>(HS0 - 2) : 0;
+#endif
+  if constexpr (TAIL >= 1) {
+    wait_vmcnt<TAIL >= 2 ? 4 + (SV ? side_stores<KIND>(HS0) : 0) + kPrevStores : 0>();
+    __builtin_amdgcn_s_barrier();
+  }
+  // DMA of chunk c+3 into the slot chunk c-1 used, one piece after each tile's MFMAs: inside the
+  // MFMA region (after the fragment reads, which the asm's memory clobber keeps ahead of it) the
+  // pieces cost 1.2K cycles per layer; issued as a block between the half-steps, 2.4K
+  auto dma = [&](auto ti) __attribute__((always_inline)) {
+    if constexpr (TAIL >= 3) chunk_dma_piece<(SLOT + 3) & 3, decltype(ti)::value>(stream, c + 3, lds_dma, voff);
+  };
+  half_step<G, false, (TAIL >= 1), 0, side_vpg<KIND>(HS0 + 1)>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0,
+                                                            lane, side1, dma);
+}
+
+// A group of NSTEP chunk-steps starting at global chunk c0 in slot SLOT0.  operand(i, kk) gives
+// the B operand of k-step 2i+kk; side(i, kk, phase) is the VALU work placed in that half-step:
+// phase 0 issues its LDS reads, phase 1 computes.
+// TAIL_END = chunks after this group (capped at 3); SV = the side work stores (training forward).
+template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, bool SV, typename Opnd, typename Side>
+__device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
+                                          uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], f32x16 (&acc)[8],
+                                          int lane, Opnd&& operand, Side&& side) {
+  static_for<NSTEP>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    constexpr int left = NSTEP - 1 - i + TAIL_END;
+    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i, SV>(
+        stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
+        operand(ic, std::integral_constant<int, 1>{}), acc, lane,
+        [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}, ph); },
+        [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 1>{}, ph); });
+  });
+}
+
+// The sample's max over both lane halves.
+__device__ __forceinline__ float sample_max(float m) { return fmaxf(m, __shfl_xor(m, 32)); }
+
+struct NoSide {
+  template <typename A, typename B, typename C>
+  __device__ __forceinline__ void operator()(A, B, C) const {}
+};
+
+template <typename I, typename K>
+__device__ __forceinline__ constexpr int kstep_of(I, K) { return 2 * I::value + K::value; }
+
+}  // namespace nerf

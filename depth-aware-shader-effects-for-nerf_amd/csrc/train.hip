@@ -19,6 +19,7 @@
 #include <utility>
 
 #include "common.h"
+#include "stream16.h"
 
 namespace nerf {
 
@@ -187,10 +188,26 @@ constexpr size_t kPackedT32Floats = tmat_offset(7) + (size_t)8 * (kDirHidden / 2
 // k index n_j = 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 (l >> 5) + (j & 3) being the
 // accumulator order in which the previous backward layer leaves its outputs (act_feature).
 // s_w = 2^(14 - e) with max |W| < 2^e per matrix (layout.h s16_exponent), and its inverse, follow.
+// The matrices lie in the order the data-gradient chain consumes them (dir_linear's h-part, then
+// trunk layers 7 .. 1), so the f16 part is one contiguous stream of 16 KiB chunks (stream16.h):
+// chunk c of the stream is at kPackedT32Floats + c * kChunkFloats.
 NERF_HD constexpr int t16_ksteps(int mt) { return mt == 7 ? kDirHidden / 16 : kHidden / 16; }
-NERF_HD constexpr size_t t16_offset(int mt) { return kPackedT32Floats + (size_t)mt * 2 * 16 * 8 * 256; }
-constexpr size_t kOffT16Consts = t16_offset(7) + (size_t)2 * 8 * 8 * 256;   // s_w[8], 1/s_w[8]
-constexpr size_t kPackedTFloats = kOffT16Consts + 16;                         // 983056
+NERF_HD constexpr size_t t16_offset(int mt) {
+  return kPackedT32Floats + (mt == 7 ? 0 : (size_t)8 * kChunkFloats + (size_t)(6 - mt) * 16 * kChunkFloats);
+}
+constexpr int kBwChunks = 8 + 7 * 16;                                         // chunks of the stream
+constexpr size_t kOffT16Consts = kPackedT32Floats + (size_t)kBwChunks * kChunkFloats;
+// constants: s_w[8], 1/s_w[8], then the data-gradient bound constants C[8] (matrix mt's largest
+// row L1 norm of W^T, x 1.0001: |W^T g| <= C max|g| rigorously) and max |density_head.weight|
+constexpr int kT16S = 0, kT16InvS = 8, kT16C = 16, kT16WsigMax = 24, kT16Consts = 32;
+constexpr size_t kPackedTFloats = kOffT16Consts + kT16Consts;                 // 983072
+NERF_HD inline void store_t16_consts(float* consts, int mt, float mx) {
+  const int e = s16_exponent(mx);
+  consts[kT16S + mt] = ldexpf(1.0f, 14 - e);
+  consts[kT16InvS + mt] = ldexpf(1.0f, e - 14);
+}
+static_assert(t16_offset(0) + 16 * kChunkFloats == kOffT16Consts && t16_offset(6) == t16_offset(7) + 8 * kChunkFloats,
+              "the transposed stream is contiguous in consumption order");
 
 NERF_HD inline float packT_value(const float* const* P, size_t e) {
   int mt = (int)(e / (8 * kActSteps * 64));
@@ -225,16 +242,12 @@ NERF_HD inline float tmat_row_max(const float* const* P, int mt, int i) {
   return m;
 }
 
-NERF_HD inline void store_t16_consts(float* consts, int mt, float mx) {
-  const int e = s16_exponent(mx);
-  consts[mt] = ldexpf(1.0f, 14 - e);
-  consts[8 + mt] = ldexpf(1.0f, e - 14);
-}
+
 
 // word w (two halves) of the split-f16 part, w relative to t16_offset(0)
 NERF_HD inline uint32_t packT16_word(const float* const* P, const float* consts, size_t w) {
-  int mt = (int)(w / (2 * 16 * 8 * 256));
-  if (mt > 7) mt = 7;
+  const size_t c = w / kChunkFloats;                    // chunk of the stream
+  const int mt = c < 8 ? 7 : 6 - (int)((c - 8) / 16);
   const size_t rel = w - (t16_offset(mt) - kPackedT32Floats);
   const int KS = t16_ksteps(mt);
   const int jj = (int)(rel & 3), lane = (int)((rel >> 2) & 63);
@@ -279,7 +292,27 @@ __global__ void __launch_bounds__(256) scaleT16_kernel(ParamPtrsT P, float* __re
 
 __global__ void scaleT16_finalize_kernel(float* __restrict__ packed) {
   const int mt = threadIdx.x;
-  if (mt < 8) store_t16_consts(packed + kOffT16Consts, mt, packed[kOffT16Consts + mt]);
+  if (mt < 8) {
+    store_t16_consts(packed + kOffT16Consts, mt, packed[kOffT16Consts + mt]);
+    packed[kOffT16Consts + kT16C + mt] *= 1.0001f;     // rounding margin on the float sums: a bound
+  }
+}
+
+// Row L1 norm of W^T (a forward input neuron's weights over the outputs) summed in order, one
+// thread per row; the matrix's maximum by atomicMax on the float bits (exact in any order: the
+// same constant as the host's).  Block 8 (a ninth matrix index) takes max |density_head.weight|.
+NERF_HD inline float tmat_row_l1(const float* const* P, int mt, int i) {
+  const int outs = mt == 7 ? kDirHidden : kHidden;
+  float l1 = 0.0f;
+  for (int o = 0; o < outs; ++o) l1 += fabsf(tmat_weight(P, mt, i, o));
+  return l1;
+}
+__global__ void __launch_bounds__(256) boundT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
+  const int mt = blockIdx.x, i = threadIdx.x;
+  float v = mt < 8 ? tmat_row_l1(P.p, mt, i) : fabsf(P.p[P_SIGMA_W][i]);
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  unsigned* c = reinterpret_cast<unsigned*>(packed + kOffT16Consts);
+  if ((threadIdx.x & 63) == 0) atomicMax(c + (mt < 8 ? kT16C + mt : kT16WsigMax), __float_as_uint(v));
 }
 
 __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
@@ -293,10 +326,12 @@ int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
   hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256)), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("packT_kernel")) return rc;
-  if (hipMemsetAsync(packedT + kOffT16Consts, 0, 8 * sizeof(float), s) != hipSuccess)
+  if (hipMemsetAsync(packedT + kOffT16Consts, 0, kT16Consts * sizeof(float), s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "packT: hipMemsetAsync failed");
   hipLaunchKernelGGL(scaleT16_kernel, dim3(kHidden / 8, 8), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("scaleT16_kernel")) return rc;
+  hipLaunchKernelGGL(boundT16_kernel, dim3(9), dim3(256), 0, s, P, packedT);
+  if (int rc = check_launch("boundT16_kernel")) return rc;
   hipLaunchKernelGGL(scaleT16_finalize_kernel, dim3(1), dim3(64), 0, s, packedT);
   if (int rc = check_launch("scaleT16_finalize_kernel")) return rc;
   const size_t words = kOffT16Consts - kPackedT32Floats;
@@ -307,11 +342,17 @@ int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
 void packT_host(const float* const* params, float* packedT) {
   for (size_t e = 0; e < kPackedT32Floats; ++e) packedT[e] = packT_value(params, e);
   float* consts = packedT + kOffT16Consts;
+  for (int k = 0; k < kT16Consts; ++k) consts[k] = 0.0f;
   for (int mt = 0; mt < 8; ++mt) {
-    float mx = 0.0f;
-    for (int i = 0; i < kHidden; ++i) mx = fmaxf(mx, tmat_row_max(params, mt, i));
+    float mx = 0.0f, l1 = 0.0f;
+    for (int i = 0; i < kHidden; ++i) {
+      mx = fmaxf(mx, tmat_row_max(params, mt, i));
+      l1 = fmaxf(l1, tmat_row_l1(params, mt, i));
+    }
     store_t16_consts(consts, mt, mx);
+    consts[kT16C + mt] = l1 * 1.0001f;
   }
+  for (int i = 0; i < kHidden; ++i) consts[kT16WsigMax] = fmaxf(consts[kT16WsigMax], fabsf(params[P_SIGMA_W][i]));
   uint32_t* words = reinterpret_cast<uint32_t*>(packedT);
   for (size_t w = 0; w < kOffT16Consts - kPackedT32Floats; ++w)
     words[kPackedT32Floats + w] = packT16_word(params, consts, w);
@@ -707,8 +748,6 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
 // stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then trunk
 // layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the kernel
 // reads M0 (as in mlp16.hip's stream).
-constexpr int kBwChunks = 8 + 7 * 16;
-
 struct BwStream {
   const char* t16;     // packedT
   const float* ring;   // LDS ring, 4 x 4096 floats
@@ -892,14 +931,311 @@ mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restr
   relu_mask_store(X, mask, gr, 0);
 }
 
+
+// ---- data gradient with split scales from a bound (f16x3, mask rows: the training path) ---------
+// mlp_backward16_lds_kernel takes each layer's split scale from the exact maximum of the layer's
+// whole gradient row, so no output can be converted before the last MFMA of the layer: the
+// epilogue (mask, row store, maximum, split) sits exposed between layers (PMC: MFMA busy 25 %,
+// 47 % of wave cycles in dependency waits).  Here the scale of d pre_{l-1} = mask . (W_l^T d pre_l)
+// comes from the bound |W_l^T g| <= C_l max|g|, C_l the largest row L1 norm of W_l^T (pack-time,
+// packedT kT16C), with max|g| the exact maximum of this layer's input, tracked while that input was
+// being converted.  So the schedule is mlp16_kernel's (stream16.h): a layer's 8 output tiles run as
+// two groups of 4 over all 16 k-steps; group A's side work converts the previous layer's tiles 4-7
+// into operands 8..15, group B's converts this layer's tiles 0-3 into operands 0..7, each a quarter
+// tile per half-step in the MFMA shadow.  A quarter: unscale, (layer 7: + dsigma w_sigma), ReLU mask
+// from the forward's mask row, one 16-byte store of the gradient row, running max, split.  A loose
+// bound only lowers the split's absolute error floor (2^-25 of the scaled unit: for a bound 2^k
+// above the row's maximum, 2^(k-39) of that maximum), far below fp32 rounding.
+// The head (rgb sigmoid, density ReLU, W_rgb^T, r_dir mask) and the dir layer's input split run
+// first on the VALU; the dir layer's inputs sit in operands 8..15 (the dir layer has 8 k-steps), so
+// its group B converts dh_7 tiles 0-3 straight into operands 0..7 for layer 7.
+constexpr int kBoLdsMask = 4 * kChunkFloats;                          // after the 4-slot ring
+constexpr int kBoLdsWsig = kBoLdsMask + 4 * 32 * kMaskRow;            // density-head weights (256)
+constexpr int kBoLdsConsts = kBoLdsWsig + kHidden;                    // packedT's 32 constants
+constexpr int kBoLdsFloats = kBoLdsConsts + kT16Consts;               // 99.6 KiB
+
+struct GradAt {                      // where a layer's d pre-activations go, and its mask
+  __amdgpu_buffer_rsrc_t rows;       // the wave's gradient rows (tail rows outside: stores dropped)
+  uint32_t loff;                     // this lane's byte offset: ((lane & 31) kGradRow + 4h) 4
+  int slice;                         // the layer's first float in the row, uniform
+  const uint32_t* mrow;              // this lane's mask words in LDS (sample row + 4h words)
+  int mlay;                          // the layer's words in the row: 8 * layer, uniform
+};
+struct BwQuarter {
+  uint32_t mw;                       // the quarter's mask word
+  f32x4 w;                           // (layer 7) density-head weights
+};
+
+template <int T0, int QG, bool SIGMA>
+__device__ __forceinline__ void bw_load4(const GradAt& g, const float* wsig, int h, BwQuarter& qv) {
+  constexpr int T = T0 + QG / 4, q = QG % 4;
+  qv.mw = g.mrow[g.mlay + T / 2];
+  if constexpr (SIGMA) qv.w = *reinterpret_cast<const f32x4*>(wsig + 32 * T + 8 * q + 4 * h);
+}
+
+// Quarter QG of a 4-tile group = registers 4q..4q+3 of output tile T0 + QG/4 -> elements 4(q&1)..+3
+// of operand in[OP0 + QG/2] (the forward's convert4 with the backward's epilogue).
+template <int T0, int OP0, int QG, bool SIGMA, bool SPLIT>
+__device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, float dsp, const BwQuarter& qv,
+                                            float s, Operand (&in)[16], float& m, const GradAt& g) {
+  constexpr int T = T0 + QG / 4, q = QG % 4;
+  constexpr int SH = 16 * (T % 2) + 4 * q;
+  f32x4 dv;
+  float xs[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float x = acc[T][4 * q + e] * inv;
+    if constexpr (SIGMA) x = fmaf(dsp, qv.w[e], x);
+    const float d = (qv.mw >> (SH + e)) & 1u ? x : 0.0f;
+    dv[e] = d;
+    if constexpr (SPLIT) {
+      m = fmaxf(m, fabsf(d));
+      xs[e] = d * s;
+    }
+  }
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows, (int)g.loff + 4 * (32 * T + 8 * q),
+                                         4 * g.slice, 0);
+  if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
+    Operand& op = in[OP0 + QG / 2];
+    typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const h16x2 hi2 = {(_Float16)xs[2 * p], (_Float16)xs[2 * p + 1]};
+      const h16x2 lo2 =
+          __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), xs[2 * p], xs[2 * p + 1]));
+      const int j = 4 * (q & 1) + 2 * p;
+      op.hi[j] = hi2[0];
+      op.hi[j + 1] = hi2[1];
+      op.lo[j] = lo2[0];
+      op.lo[j + 1] = lo2[1];
+    }
+  }
+}
+
+template <int PH, int T0, int OP0, int QG, bool SIGMA, bool SPLIT>
+__device__ __forceinline__ void bw_quarter(const f32x16 (&acc)[8], float inv, float dsp, const float* wsig, int h,
+                                           float s, Operand (&in)[16], float& m, BwQuarter& qv, const GradAt& g) {
+  if constexpr (PH == 0) bw_load4<T0, QG, SIGMA>(g, wsig, h, qv);
+  else bw_convert4<T0, OP0, QG, SIGMA, SPLIT>(acc, inv, dsp, qv, s, in, m, g);
+}
+
+__global__ void __launch_bounds__(64 * kW16Waves, 1)
+mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
+                            const uint32_t* __restrict__ masks, const float* __restrict__ sigma,
+                            const float* __restrict__ rgb, const float* __restrict__ dsigma,
+                            const float* __restrict__ drgb, int64_t M, float* __restrict__ grad) {
+  __shared__ __attribute__((aligned(16))) float lds[kBoLdsFloats];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
+  // every wave runs to the end (the weight stream has barriers); tail lanes repeat sample M-1 and
+  // store nothing
+  const bool valid = s0 + (lane & 31) < M;
+  const int64_t s = imin64(s0 + (lane & 31), M - 1);
+  const int64_t rows_here = s0 < M ? imin64(M - s0, 32) : 0;
+  GradAt ga;
+  ga.rows = __builtin_amdgcn_make_buffer_rsrc(grad + imin64(s0, M) * kGradRow, (short)0, (int)(rows_here * kGradRow * 4),
+                                              0x00020000);
+  ga.loff = valid ? ((uint32_t)(lane & 31) * kGradRow + 4 * h) * 4 : 0x40000000u;
+  // the wave's 32 mask rows (8,704 contiguous bytes) into LDS; constants and w_sigma
+  uint32_t* mwave = reinterpret_cast<uint32_t*>(lds + kBoLdsMask) + wave * 32 * kMaskRow;
+  for (int i = lane; i < 32 * kMaskRow / 4; i += 64) {
+    const int row = i / (kMaskRow / 4), c = i % (kMaskRow / 4);
+    reinterpret_cast<u32x4*>(mwave)[i] = reinterpret_cast<const u32x4*>(masks + imin64(s0 + row, M - 1) * kMaskRow)[c];
+  }
+  if (threadIdx.x < kHidden / 4)
+    reinterpret_cast<f32x4*>(lds + kBoLdsWsig)[threadIdx.x] = reinterpret_cast<const f32x4*>(packed + kOffSigmaW)[threadIdx.x];
+  if (threadIdx.x < kT16Consts) lds[kBoLdsConsts + threadIdx.x] = packedT[kOffT16Consts + threadIdx.x];
+  ga.mrow = mwave + (lane & 31) * kMaskRow + 4 * h;
+  ga.mlay = 0;
+  ga.slice = 0;
+
+  // heads (models.py:137-160 differentiated): rgb = sigmoid(v) -> dv = drgb rgb (1 - rgb); density
+  // sigma = ReLU(v_s) -> d v_s = dsigma [sigma > 0]
+  float dv[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float y = rgb[3 * s + c];
+    dv[c] = drgb[3 * s + c] * (y * (1.0f - y));
+  }
+  const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
+  const float* wr = packed + kOffRgbW;
+  float dhd[4][16];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = t * 32 + 8 * q + 4 * h + e;
+        dhd[t][4 * q + e] = fmaf(dv[2], wr[2 * kDirHidden + n], fmaf(dv[1], wr[kDirHidden + n], dv[0] * wr[n]));
+      }
+  __syncthreads();                    // mask rows, w_sigma and constants in LDS
+  const float* cst = lds + kBoLdsConsts;
+  const float* wsig = lds + kBoLdsWsig;
+  float* grow = grad + s * kGradRow;
+  if (valid && h == 0) {
+    grow[kGradSigma] = dsp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+  }
+  // d hd rows; d pre_dir = d hd [r_dir > 0] (hd = ReLU(dir pre) + appearance): rows, max, split at
+  // the exact maximum into operands 8..15 (the dir layer's 8 k-steps)
+  Operand in[16];
+  float m_dir = 0.0f;
+  {
+    const uint32_t* md = mwave + (lane & 31) * kMaskRow + (kMaskRDirByte + 8 * h) / 4;
+    const uint32_t mk[2] = {md[0], md[1]};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 a, b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = dhd[t][4 * q + e];
+          b[e] = (mk[t / 2] >> (16 * (t % 2) + 4 * q + e)) & 1u ? a[e] : 0.0f;
+          dhd[t][4 * q + e] = b[e];
+          m_dir = fmaxf(m_dir, fabsf(b[e]));
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows,
+                                               (int)ga.loff + 4 * (kGradHd + 32 * t + 8 * q), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), ga.rows,
+                                               (int)ga.loff + 4 * (kGradDir + 32 * t + 8 * q), 0, 0);
+      }
+  }
+  m_dir = sample_max(m_dir);
+  const float s_dir = pow2_scale(m_dir);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split_into(dhd[t][4 * q + e] * s_dir, in[8 + 2 * t + q / 2], 4 * (q & 1) + e);
+  // d pre_7's scale: |W_dh^T g + dsigma w_sigma| <= C_dir max|g| + |dsigma| max|w_sigma|
+  float s_cur = pow2_scale(cst[kT16C + 7] * m_dir + fabsf(dsp) * cst[kT16WsigMax]);
+  float inv_prev = cst[kT16InvS + 7] / s_dir;
+
+  // the weight stream: W^T fragments of dir_linear's h-part, then trunk layers 7 .. 1
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_sched_barrier(0);
+  const float* stream = packedT + kPackedT32Floats;
+  const uint32_t lds_dma = (uint32_t)(uintptr_t)(lptr_t)lds + 1024u * wave;
+  const uint32_t voff = 16u * lane + 1024u * wave;
+  chunk_dma<0>(stream, 0, lds_dma, voff);
+  chunk_dma<1>(stream, 1, lds_dma, voff);
+  chunk_dma<2>(stream, 2, lds_dma, voff);
+  wait_vmcnt<8>();
+  __builtin_amdgcn_s_barrier();
+  h16x8 a0[4][2], a1[4][2];
+  read_kstep<0>(lds, a0, lane);
+  f32x16 acc[8];
+  float m = 0.0f;
+  BwQuarter qv[2];
+  using Yes = std::true_type;
+  using No = std::false_type;
+
+  // ---- dir layer: d h_7 = W_dh^T d pre_dir (8 k-steps, operands 8..15), 4 chunk-steps per group;
+  // group B converts group A's tiles 0-3 (+ dsigma w_sigma, mask_7) into operands 0..7, two
+  // quarters per half-step
+  auto dir_operand = [&](auto i, auto kk) -> const Operand& { return in[8 + kstep_of(i, kk)]; };
+  run_group<0, 4, 0, 3, kSideNone, true>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, dir_operand, NoSide{});
+  GradAt g_cur = ga, g_prev = ga;
+  g_cur.slice = 7 * kHidden;
+  g_cur.mlay = (kMaskLayerBytes / 4) * 7;
+  run_group<1, 4, 0, 3, kSideHalf, true>(stream, 4, lds, lds_dma, voff, a0, a1, acc, lane, dir_operand,
+                                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                           constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
+                                           bw_quarter<P, 0, 0, 2 * hs, true, true>(acc, inv_prev, dsp, wsig, h, s_cur,
+                                                                                     in, m, qv[0], g_cur);
+                                           bw_quarter<P, 0, 0, 2 * hs + 1, true, true>(acc, inv_prev, dsp, wsig, h,
+                                                                                         s_cur, in, m, qv[1], g_cur);
+                                         });
+
+  // ---- trunk layers l = 7 .. 1: d h_{l-1} = W_l^T d pre_l.  On entry operands 0..7 hold d pre_l
+  // tiles 0-3 split at s_cur, d h_l tiles 4-7 wait in acc[4..7] (unscaled by inv_prev), m holds the
+  // max of d pre_l tiles 0-3.  Side-work schedule: mlp16_kernel's (kSidePrev / kSideCur).
+  auto act_operand = [&](auto i, auto kk) -> const Operand& { return in[kstep_of(i, kk)]; };
+  // group A's side: d pre_l tiles 4-7 (SG: layer 7 adds dsigma w_sigma)
+  auto side_prev = [&](auto i, auto kk, auto ph, auto sg_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
+    constexpr bool sg = decltype(sg_tag)::value;
+    if constexpr (hs == 0) {
+      bw_quarter<P, 4, 8, 0, sg, true>(acc, inv_prev, dsp, wsig, h, s_cur, in, m, qv[0], g_prev);
+      bw_quarter<P, 4, 8, 1, sg, true>(acc, inv_prev, dsp, wsig, h, s_cur, in, m, qv[1], g_prev);
+    } else if constexpr (hs <= 14) {
+      bw_quarter<P, 4, 8, hs + 1, sg, true>(acc, inv_prev, dsp, wsig, h, s_cur, in, m, qv[0], g_prev);
+    }
+  };
+  float s_nxt = 0.0f, inv_cur = 0.0f;
+  // group B's side: d pre_{l-1} tiles 0-3 (SP: split for the next layer; layer 0 has no consumer)
+  auto side_cur = [&](auto i, auto kk, auto ph, auto sp_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
+    constexpr bool sp = decltype(sp_tag)::value;
+    if constexpr (hs >= 1 && hs <= 14) {
+      bw_quarter<P, 0, 0, hs - 1, false, sp>(acc, inv_cur, 0.0f, wsig, h, s_nxt, in, m, qv[0], g_cur);
+    } else if constexpr (hs == 15) {
+      bw_quarter<P, 0, 0, 14, false, sp>(acc, inv_cur, 0.0f, wsig, h, s_nxt, in, m, qv[0], g_cur);
+      bw_quarter<P, 0, 0, 15, false, sp>(acc, inv_cur, 0.0f, wsig, h, s_nxt, in, m, qv[1], g_cur);
+    }
+  };
+  auto layer = [&](int l, auto sg_tag, auto last_tag) __attribute__((always_inline)) {
+    constexpr bool last = decltype(last_tag)::value;
+    const int c0 = 8 + (7 - l) * 16;
+    g_prev.slice = l * kHidden;
+    g_prev.mlay = (kMaskLayerBytes / 4) * l;
+    g_cur.slice = (l - 1) * kHidden;
+    g_cur.mlay = (kMaskLayerBytes / 4) * (l - 1);
+    inv_cur = cst[kT16InvS + l - 1] / s_cur;
+    run_group<0, 8, 0, 3, kSidePrev, true>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                                           [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                             side_prev(i, kk, ph, sg_tag);
+                                           });
+    // the inputs of this layer are complete: the scale of d pre_{l-1} from the bound
+    m = sample_max(m);
+    s_nxt = pow2_scale(cst[kT16C + l - 1] * m);
+    m = 0.0f;
+    if constexpr (last) {
+      run_group<1, 8, 0, 0, kSideCur, true>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                              side_cur(i, kk, ph, No{});
+                                            });
+    } else {
+      run_group<1, 8, 0, 3, kSideCur, true>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                              side_cur(i, kk, ph, Yes{});
+                                            });
+    }
+    inv_prev = inv_cur;
+    s_cur = s_nxt;
+  };
+  layer(7, Yes{}, No{});
+#pragma unroll 1
+  for (int l = 6; l >= 2; --l) layer(l, No{}, No{});
+  layer(1, No{}, Yes{});
+  // d pre_0 tiles 4-7: exposed (no MFMA left to hide behind)
+  g_prev.slice = 0;
+  g_prev.mlay = 0;
+  static_for<16>([&](auto qc) __attribute__((always_inline)) {
+    constexpr int QG = decltype(qc)::value;
+    bw_quarter<0, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
+    bw_quarter<1, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
+  });
+}
+
 int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
                         const float* sigma, const float* rgb, const float* dsigma, const float* drgb, int64_t M,
                         float* grad, hipStream_t s) {
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3) {
+#ifdef NERF_BW_EXACT_MAX   // A/B build: the exact-row-maximum kernel
     if (masks)
       hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
+#else
+    if (masks)
+      hipLaunchKernelGGL(mlp_backward16_bound_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
+                         packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
+#endif
     else
       hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, save, sigma, rgb, dsigma, drgb, M, grad);

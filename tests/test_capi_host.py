@@ -374,7 +374,7 @@ def tfrag_matrix(packedT, mt):
 
 def test_transposed_fragments_are_permuted_weight_transposes(ref_state):
     packedT = host_pack_transposed(ref_state)
-    assert packedT.size == 2 * (7 * 256 * 256 + 256 * 128) + 16
+    assert packedT.size == 2 * (7 * 256 * 256 + 256 * 128) + 32
     for layer in range(1, 8):
         W = ref_state[f"pts_linears.{layer}.weight"].numpy()[:, :256]        # [out][in]
         cols = [act_feature(s // 2, s % 2) for s in range(256)]
@@ -385,15 +385,17 @@ def test_transposed_fragments_are_permuted_weight_transposes(ref_state):
 
 
 def test_transposed_split_f16_fragments(ref_state):
-    """The split-f16 part of packedT (mlp_backward16_kernel): per matrix a power-of-two s_w with
-    max |W s_w| < 2^14, hi = f16(W s_w) and lo = f16(W s_w - hi) in fragment order
-    [group][k-step][tile][hi, lo][lane][8 halves], k index 32 (ks>>1) + 16 (ks&1) + 8 (j>>2) + 4 h + (j&3)."""
+    """The split-f16 part of packedT (the data-gradient chain's weight stream): per matrix a
+    power-of-two s_w with max |W s_w| < 2^14, hi = f16(W s_w) and lo = f16(W s_w - hi) in fragment
+    order [group][k-step][tile][hi, lo][lane][8 halves], k index 32 (ks>>1) + 16 (ks&1) + 8 (j>>2) +
+    4 h + (j&3); the matrices in consumption order (dir_linear's h-part, then trunk layers 7 .. 1);
+    then the bound constants: each matrix's largest row L1 norm of W^T (x 1.0001) and max |w_sigma|."""
     packedT = host_pack_transposed(ref_state)
     base = 7 * 256 * 256 + 256 * 128
-    consts = packedT[2 * base: 2 * base + 16]
+    consts = packedT[2 * base: 2 * base + 32]
     words = packedT[base: 2 * base].view(np.float16)
     off = 0
-    for mt in range(8):
+    for mt in (7, 6, 5, 4, 3, 2, 1, 0):
         if mt < 7:
             W = ref_state[f"pts_linears.{mt + 1}.weight"].numpy()[:, :256]       # [out][in]
         else:
@@ -414,6 +416,9 @@ def test_transposed_split_f16_fragments(ref_state):
         hi, lo = blk[:, :, :, 0], blk[:, :, :, 1]
         assert np.array_equal(hi, exp.astype(np.float16).astype(np.float64)), mt
         assert np.abs(hi + lo - exp).max() <= 2.0 ** -10, mt      # |W s_w| < 2^14: split residual < 2^-11
+        l1 = np.abs(WT).sum(1).max()
+        assert l1 <= consts[16 + mt] <= l1 * 1.0002, mt              # rigorous bound: |W^T g| <= C max|g|
+    assert consts[24] == np.abs(ref_state["density_head.weight"].numpy()).max()
 
 
 def emulate_backward(packed, packedT, x, d, app, g_rgb, g_sigma):

@@ -284,18 +284,22 @@ def test_wgrad_generic_shapes():
         else:
             # sums of 50K-262K products: an entry near 0 by cancellation has no relative accuracy in any
             # fp32 order, so each entry's error is measured against its sum of |terms| (the scale of
-            # an fp32 summation's error), and the whole against the CPU fp32 GEMM's rel-L2 error
+            # an fp32 summation's error): every entry within 1e-6 of it, and the max and p99.9 of that
+            # per-entry error no worse than twice the CPU fp32 GEMM's (a regression in the bf16x6
+            # split or the chunk reduction shows up there first)
             ad, xd = a[:, :N].abs().double(), x[idx, :K].abs().double()
             mag_w, mag_b = (ad.T @ xd).numpy(), ad.sum(0).numpy()
             cpu_w = (a[:, :N].T @ x[idx, :K]).double().numpy()
             cpu_b = a[:, :N].sum(0).double().numpy()
             for got, exp, mag, cpu, name in ((ow.cpu().numpy() / 2, exp_w, mag_w, cpu_w, "w"),
                                              (ob.cpu().numpy() / 2, exp_b, mag_b, cpu_b, "b")):
-                err = float((np.abs(got - exp) / mag).max())
-                assert err <= 1e-6, (M, N, K, name, err)
-                e_gpu = np.linalg.norm(got - exp) / np.linalg.norm(mag)
-                e_cpu = np.linalg.norm(cpu - exp) / np.linalg.norm(mag)
-                assert e_gpu <= max(4 * e_cpu, 1e-7), (M, N, K, name, e_gpu, e_cpu)
+                r_gpu = (np.abs(got - exp) / mag).ravel()
+                r_cpu = (np.abs(cpu - exp) / mag).ravel()
+                assert r_gpu.max() <= 1e-6, (M, N, K, name, r_gpu.max())
+                for stat, f in (("max", np.max), ("p99.9", lambda v: np.quantile(v, 0.999))):
+                    g_, c_ = float(f(r_gpu)), float(f(r_cpu))
+                    print(f"wgrad M={M} N={N} K={K} {name} {stat}: gpu {g_:.3g} cpu {c_:.3g}")
+                    assert g_ <= 2 * c_ + 1e-9, (M, N, K, name, stat, g_, c_)
 
 
 def test_adam_matches_torch():
