@@ -195,14 +195,16 @@ constexpr int kMaskRowBytes = kMaskRDirByte + 16;            // 272
 constexpr int kMaskRow = kMaskRowBytes / 4;                  // 68 words per sample
 
 // Per-sample gradient row written by the backward pass (nerf_mlp_backward):
-//   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dhd (128) | drgb_pre (3) + pad | dsigma_pre + pad]
+//   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dsigma_pre + pad | dhd (128) | drgb_pre (3) + pad]
 // dpre_l = d loss / d (pre-activation of trunk layer l), dhd = d loss / d hd.  Every slice starts
-// on a 16-byte boundary (the weight-gradient GEMM streams them with 16-byte loads).
+// on a 16-byte boundary (the weight-gradient GEMM streams them with 16-byte loads).  dsigma_pre
+// follows dpre_dir: both heads read h7, so their weight gradients run as one 129-row GEMM over
+// [h7 | enc_d] (param_grads), which reads h7 once.
 constexpr int kGradDir = 8 * kHidden;                        // 2048
-constexpr int kGradHd = kGradDir + kDirHidden;               // 2176
-constexpr int kGradRgb = kGradHd + kDirHidden;               // 2304
-constexpr int kGradSigma = kGradRgb + 4;                     // 2308
-constexpr int kGradRow = kGradSigma + 4;                     // 2312
+constexpr int kGradSigma = kGradDir + kDirHidden;            // 2176
+constexpr int kGradHd = kGradSigma + 4;                      // 2180
+constexpr int kGradRgb = kGradHd + kDirHidden;               // 2308
+constexpr int kGradRow = kGradRgb + 4;                       // 2312
 
 // Float offset, inside matrix m's fragment array, of element j of lane `lane` in the
 // fragment block (n-tile nt, k-step quad kq): ks = 4*kq + j.

@@ -298,21 +298,38 @@ __global__ void scaleT16_finalize_kernel(float* __restrict__ packed) {
   }
 }
 
-// Row L1 norm of W^T (a forward input neuron's weights over the outputs) summed in order, one
-// thread per row; the matrix's maximum by atomicMax on the float bits (exact in any order: the
-// same constant as the host's).  Block 8 (a ninth matrix index) takes max |density_head.weight|.
-NERF_HD inline float tmat_row_l1(const float* const* P, int mt, int i) {
-  const int outs = mt == 7 ? kDirHidden : kHidden;
+// Row L1 norm of W^T (a forward input neuron's weights over the outputs): four partial sums over
+// the output quarters, each in order, added in order (the host's tmat_row_l1 is the same
+// expression, so device and host constants are bit-identical); the matrix's maximum by atomicMax on
+// the float bits (exact in any order).  One block per (matrix, 64 rows): thread = (row, quarter).
+// Block 32 takes max |density_head.weight|.
+NERF_HD inline float tmat_row_l1_part(const float* const* P, int mt, int i, int q) {
+  const int outs = mt == 7 ? kDirHidden : kHidden, per = outs / 4;
   float l1 = 0.0f;
-  for (int o = 0; o < outs; ++o) l1 += fabsf(tmat_weight(P, mt, i, o));
+  for (int o = q * per; o < (q + 1) * per; ++o) l1 += fabsf(tmat_weight(P, mt, i, o));
   return l1;
 }
+NERF_HD inline float tmat_row_l1(const float* const* P, int mt, int i) {
+  return ((tmat_row_l1_part(P, mt, i, 0) + tmat_row_l1_part(P, mt, i, 1)) + tmat_row_l1_part(P, mt, i, 2)) +
+         tmat_row_l1_part(P, mt, i, 3);
+}
 __global__ void __launch_bounds__(256) boundT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
-  const int mt = blockIdx.x, i = threadIdx.x;
-  float v = mt < 8 ? tmat_row_l1(P.p, mt, i) : fabsf(P.p[P_SIGMA_W][i]);
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  __shared__ float part[4][64];
   unsigned* c = reinterpret_cast<unsigned*>(packed + kOffT16Consts);
-  if ((threadIdx.x & 63) == 0) atomicMax(c + (mt < 8 ? kT16C + mt : kT16WsigMax), __float_as_uint(v));
+  if (blockIdx.x == 32) {
+    float v = fabsf(P.p[P_SIGMA_W][threadIdx.x]);
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(c + kT16WsigMax, __float_as_uint(v));
+    return;
+  }
+  const int mt = blockIdx.x >> 2, r = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int i = (blockIdx.x & 3) * 64 + r;
+  part[q][r] = tmat_row_l1_part(P.p, mt, i, q);
+  __syncthreads();
+  if (q != 0) return;
+  float v = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  if (r == 0) atomicMax(c + kT16C + mt, __float_as_uint(v));
 }
 
 __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
@@ -330,7 +347,7 @@ int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
     return set_error(NERF_ERR_HIP, "packT: hipMemsetAsync failed");
   hipLaunchKernelGGL(scaleT16_kernel, dim3(kHidden / 8, 8), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("scaleT16_kernel")) return rc;
-  hipLaunchKernelGGL(boundT16_kernel, dim3(9), dim3(256), 0, s, P, packedT);
+  hipLaunchKernelGGL(boundT16_kernel, dim3(33), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("boundT16_kernel")) return rc;
   hipLaunchKernelGGL(scaleT16_finalize_kernel, dim3(1), dim3(64), 0, s, packedT);
   if (int rc = check_launch("scaleT16_finalize_kernel")) return rc;
@@ -743,8 +760,10 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
 // software-pipelined as in the forward's stream: a step's MFMAs run while the next step's 8
 // fragments are read, and the barrier that publishes chunk g+1 sits between chunk g's two steps:
 //   [read step 2c+1 (slot g) | MFMA step 2c] wait DMA(g+1), barrier, DMA(g+3) into the slot of
-//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]
-// (every read of chunk g-1 fed an MFMA issued before this barrier, so its slot is free).  The
+//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]   -- i.e. bw_publish(g+1) issues
+//   DMA((g+1)+2) into chunk (g+1)-2's slot
+// (two chunks ahead in a 4-slot ring: every wave's reads of chunk g-2 fed MFMAs issued before the
+// publish(g) barrier, so DMA(g+2), issued right after that barrier, overwrites a free slot).  The
 // stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then trunk
 // layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the kernel
 // reads M0 (as in mlp16.hip's stream).
@@ -993,8 +1012,10 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
       xs[e] = d * s;
     }
   }
+#ifndef NERF_BW_NO_STORES   // (timing-only A/B build: the cost of the gradient-row stores)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows, (int)g.loff + 4 * (32 * T + 8 * q),
                                          4 * g.slice, 0);
+#endif
   if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
     Operand& op = in[OP0 + QG / 2];
     typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
@@ -1345,7 +1366,7 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   constexpr int AC4 = BN / 4, XC4 = BK / 4;        // float4 columns per staged row
   __shared__ float As[2][kWS][APAD];
   __shared__ float Xs[2][kWS][XPAD];
-  __shared__ float bsum[256 / AC4][BN];
+  __shared__ double bsum[256 / AC4][BN];
   const int b = blockIdx.x;
   const int grp = b / (8 * tiles), rem = b % (8 * tiles);
   const int chunk = grp * 8 + (rem & 7);
@@ -1363,7 +1384,7 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   constexpr int AROWS = 256 / AC4, XROWS = 256 / XC4;   // rows per pass
   const int a_valid = N - (n0 + a_c), x_valid = K - (k0 + x_c);
   f32x4 ra[WN], rx[WK];
-  f32x4 bacc = {0.0f, 0.0f, 0.0f, 0.0f};
+  double bacc[4] = {0.0, 0.0, 0.0, 0.0};      // bias column in double: one rounding per chunk
   const f32x4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
   auto load = [&](int64_t mb) __attribute__((always_inline)) {
     sfor<WN>([&](auto pc) __attribute__((always_inline)) {
@@ -1382,7 +1403,10 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
     sfor<WN>([&](auto pc) __attribute__((always_inline)) {
       constexpr int p = decltype(pc)::value;
       *reinterpret_cast<f32x4*>(&As[buf][a_r + AROWS * p][a_c]) = ra[p];
-      if (do_bias) bacc += ra[p];
+      if (do_bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bacc[e] += (double)ra[p][e];
+      }
     });
     sfor<WK>([&](auto pc) __attribute__((always_inline)) {
       constexpr int p = decltype(pc)::value;
@@ -1431,13 +1455,14 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   emit(acc11, 1, 1);
   if (do_bias) {
     // every staged a row passed through store() exactly once (the prologue stores stage 0)
-    *reinterpret_cast<f32x4*>(&bsum[a_r][a_c]) = bacc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bsum[a_r][a_c + e] = bacc[e];
     __syncthreads();
     if (tid < BN && n0 + tid < N) {
-      float sum = 0.0f;
+      double sum = 0.0;
 #pragma unroll
       for (int r = 0; r < AROWS; ++r) sum += bsum[r][tid];
-      out[(size_t)(n0 + tid) * KP + K] = sum;
+      out[(size_t)(n0 + tid) * KP + K] = (float)sum;
     }
   }
 }
@@ -1476,7 +1501,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   constexpr int SX = 2 * BK / 256 > 0 ? 2 * BK / 256 : 1;
   __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BN][kBfRow];
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BK][kBfRow];
-  __shared__ float bsum[2][BN];
+  __shared__ double bsum[2][BN];
   const int b = blockIdx.x;
   const int grp = b / (8 * tiles), rem = b % (8 * tiles);
   const int chunk = grp * 8 + (rem & 7);
@@ -1489,9 +1514,9 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wn = w % WN, wk = w / WN;
   float ra[2][SA][8], rx[2][SX][8];   // two stages in flight: stage k's values in set k % 2
-  float bacc[SA];
+  double bacc[SA];                   // bias column in double: one rounding per chunk
 #pragma unroll
-  for (int q = 0; q < SA; ++q) bacc[q] = 0.0f;
+  for (int q = 0; q < SA; ++q) bacc[q] = 0.0;
   // Operands through buffer loads (an out-of-range offset reads 0, so no branches in the loader).
   // a: one resource per stage, based at the stage's first row, sized to the chunk's remaining rows;
   // a slot's sample j sits at byte aoff + j*lda4 (past the resource for samples >= m1), and a
@@ -1595,7 +1620,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
       if (slot < 2 * BN) {
         if (do_bias) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bacc[q] += ra[SET][q][j];
+          for (int j = 0; j < 8; ++j) bacc[q] += (double)ra[SET][q][j];
         }
         split_store(ra[SET][q], &As[buf][0][0], col, oct, BN);
       }
@@ -1677,7 +1702,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
       if (slot < 2 * BN) bsum[oct][col] = bacc[q];
     }
     __syncthreads();
-    if (tid < BN && n0 + tid < N) out[(size_t)(n0 + tid) * KP + K] = bsum[0][tid] + bsum[1][tid];
+    if (tid < BN && n0 + tid < N) out[(size_t)(n0 + tid) * KP + K] = (float)(bsum[0][tid] + bsum[1][tid]);
   }
 }
 
@@ -1711,7 +1736,7 @@ __global__ void __launch_bounds__(512, 1)
 wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
                    int clen, float* __restrict__ partial) {
   __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
-  __shared__ float bsum[2][kWT];
+  __shared__ double bsum[2][kWT];
   const int chunk = blockIdx.x;
   const int64_t m0 = (int64_t)chunk * clen;
   const int64_t m1 = m0 + clen < M ? m0 + clen : M;
@@ -1728,7 +1753,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   for (int t = 0; t < 2; ++t) xvo[t] = (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)(64 * wk + 32 * t + c);
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
   float ra[2][8], rx[2][2][8];   // two stages in flight: stage k's values in set k % 2
-  float bacc = 0.0f;
+  double bacc = 0.0;                 // bias column in double: one rounding per chunk
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
@@ -1748,7 +1773,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += ra[SET][j];
+    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
     bf16x8 p0, p1, p2;
     split3_bf16(ra[SET], p0, p1, p2);
     *reinterpret_cast<bf16x8*>(&As[buf][0][col][8 * oct]) = p0;
@@ -1817,7 +1842,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   // bias column: every staged a value passed through store_a() exactly once (the rest are zeros)
   bsum[oct][col] = bacc;
   __syncthreads();
-  if (tid < kWT) out[(size_t)tid * KP + kWT] = bsum[0][tid] + bsum[1][tid];
+  if (tid < kWT) out[(size_t)tid * KP + kWT] = (float)(bsum[0][tid] + bsum[1][tid]);
 }
 
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
@@ -1844,7 +1869,7 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   const uint32_t xvo = xc < K ? (uint32_t)(2 * xp) * ldx4 + 4u * (uint32_t)xc : 0x80000000u;
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
   float ra[2][8], rx[2][2];
-  float bacc = 0.0f;
+  double bacc = 0.0;                 // bias column in double: one rounding per chunk
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
@@ -1894,7 +1919,7 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     const int buf = SET;
     bf16x8 fa[3];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += ra[SET][j];
+    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
     split3_bf16(ra[SET], fa[0], fa[1], fa[2]);
     load(set_c, st + 2);
     __builtin_amdgcn_sched_barrier(0);
@@ -1930,7 +1955,7 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   }
   // bias column: this lane summed column 32w + c over its 8 samples of every stage
   bacc += __shfl_xor(bacc, 32);
-  if (h == 0) out[(size_t)(32 * w + c) * KP + K] = bacc;
+  if (h == 0) out[(size_t)(32 * w + c) * KP + K] = (float)bacc;
 }
 
 template <int WN, int WK>
@@ -1948,12 +1973,20 @@ static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, i
   return check_launch("wgrad_bf_kernel");
 }
 
+struct WgradSplit {                  // rows n >= n0 of a weight gradient belong to a second parameter
+  int n0 = 0;
+  float* out_w = nullptr;            // its weight gradient, ld ldo, the first k columns
+  int ldo = 0, k = 0;
+  float* out_b = nullptr;            // its bias gradient (the bias column), nullable
+};
+
 // out_w[n][k] (ld K) and out_b[n] (nullable) = (accumulate ? out : 0) + sum over chunks, in chunk
-// order.  A workgroup owns 64 float4 columns of the partial layout; its 4 waves each sum a
+// order; with a WgradSplit, rows n >= split.n0 go to split.out_w[n - n0][k < split.k] and
+// split.out_b[n - n0] instead.  A workgroup owns 64 float4 columns of the partial layout; its 4 waves each sum a
 // quarter of the chunks (fixed order), then the quarters are added in order: deterministic.
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w, int ldo,
-                    float* __restrict__ out_b, int accumulate) {
+                    float* __restrict__ out_b, int accumulate, WgradSplit split) {
   __shared__ f32x4 part[4][64];
   const int KP = K + 1;
   const int64_t stride = wgrad_stride(N, K);
@@ -1984,7 +2017,13 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
     const int64_t idx = col4 * 4 + e;
     if (idx >= (int64_t)N * KP) break;
     const int n = (int)(idx / KP), k = (int)(idx % KP);
-    float* dst = k < K ? out_w + (size_t)n * ldo + k : (out_b ? out_b + n : nullptr);
+    float* dst;
+    if (split.out_w && n >= split.n0) {   // rows from n0 on belong to a second output (WgradSplit)
+      const int n2 = n - split.n0;
+      dst = k < split.k ? split.out_w + (size_t)n2 * split.ldo + k : (k == K && split.out_b ? split.out_b + n2 : nullptr);
+    } else {
+      dst = k < K ? out_w + (size_t)n * ldo + k : (out_b ? out_b + n : nullptr);
+    }
     if (dst) *dst = accumulate ? *dst + sum[e] : sum[e];
   }
 }
@@ -2007,7 +2046,8 @@ static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, 
 }
 
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
-                 float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s) {
+                 float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
+                 const WgradSplit* split = nullptr) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
@@ -2038,7 +2078,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (rc) return rc;
   const int64_t cols4 = wgrad_stride(N, K) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(256), 0, s, ws, chunks, N, K,
-                     out_w, ldo, out_b, accumulate);
+                     out_w, ldo, out_b, accumulate, split ? *split : WgradSplit{});
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -2283,8 +2323,6 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
       {grad + 5 * kHidden, kHidden, save + save_h(4), kHidden, 10, 0, kHidden, true},
       {grad + 6 * kHidden, kHidden, save + save_h(5), kHidden, 12, 0, kHidden, true},
       {grad + 7 * kHidden, kHidden, save + save_h(6), kHidden, 14, 0, kHidden, true},
-      {grad + kGradSigma, 1, save + save_h(7), kHidden, P_SIGMA_W, 0, kHidden, true},
-      {grad + kGradDir, kDirHidden, save + save_h(7), kHidden + kDirEnc, P_DIR_W, 0, kHidden + kDirEnc, true},  // [h7 | enc_d]
       {grad + kGradRgb, 3, save + kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true},
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
@@ -2295,6 +2333,16 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
                            0, ws, s)))
       return rc;
   }
+  // dir_linear (128 rows over [h7 | enc_d]) and the density head (1 row over h7) in one GEMM: the
+  // gradient row holds [d pre_dir | d sigma], so rows 0..127 are dir_linear's gradient and row 128
+  // (its first 256 columns and the bias column) the density head's: h7 is read once
+  static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
+  if (wgrad_workspace_floats(M, kDirHidden + 1, kHidden + kDirEnc) > ws_floats)
+    return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+  const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B]};
+  if ((rc = launch_wgrad(grad + kGradDir, kGradRow, kDirHidden + 1, save + save_h(7), kSaveRow, kHidden + kDirEnc, 1, M,
+                         g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads)))
+    return rc;
   if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
     return NERF_OK;
   }

@@ -120,7 +120,9 @@ class NeRFDataset(_RayBatches):
 
     def _image_chw(self, idx):
         """ToTensor of the image file (dataset.py:156-161): rgb (3,H,W) in [0,1], alpha (1,H,W)
-        (ones without an alpha channel; None for the custom format, dataset.py:182,190)."""
+        (ones without an alpha channel; None for the custom format, dataset.py:182,190).  The decoded
+        file is cached as its uint8 HWC array (a quarter of the float tensor's size; the reference
+        decodes on every access) and converted on every call, so callers get fresh tensors."""
         if idx not in self._cache:
             from PIL import Image
             with Image.open(self.paths[idx]) as img:
@@ -129,14 +131,15 @@ class NeRFDataset(_RayBatches):
                 arr = np.asarray(img, dtype=np.uint8)
             if arr.ndim == 2:
                 arr = arr[..., None]
-            t = torch.from_numpy(arr.copy()).permute(2, 0, 1).float().div(255)   # ToTensor
-            rgb = t[:3]
-            if self.dataset_type != "nerf_synthetic":
-                alpha = None
-            else:
-                alpha = t[3:4] if t.shape[0] == 4 else torch.ones_like(t[:1])
-            self._cache[idx] = (rgb, alpha)
-        return self._cache[idx]
+            self._cache[idx] = np.ascontiguousarray(arr)
+        arr = self._cache[idx]
+        t = torch.from_numpy(arr).permute(2, 0, 1).float().div(255)              # ToTensor
+        rgb = t[:3]
+        if self.dataset_type != "nerf_synthetic":
+            alpha = None
+        else:
+            alpha = t[3:4] if t.shape[0] == 4 else torch.ones_like(t[:1])
+        return rgb, alpha
 
     def _pixels(self, idx, sel, o, d):
         rgb, alpha = self._image_chw(idx)

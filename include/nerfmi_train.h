@@ -27,7 +27,7 @@ extern "C" {
 
 /* Per-sample rows the forward saves / the backward writes (floats). */
 #define NERF_SAVE_ROW 2400 /* [h0..h3 | enc_x(64) | h4..h7 | enc_d(32) | r_dir(128) | hd(128)] */
-#define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dhd(128) | drgb(3)+pad | dsigma+pad] */
+#define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dsigma+pad | dhd(128) | drgb(3)+pad] */
 /* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):
  * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes (csrc/layout.h kMaskRow). */
 #define NERF_MASK_ROW 68

@@ -179,7 +179,12 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
                                       L.ptr(ggs), L.ptr(ggr), M, L.ptr(grad2), s), "bwd")
     torch.cuda.synchronize()
     if f16:
-        assert torch.equal(grad, grad2)
+        # the mask-row kernel splits each layer's gradient at a scale from a bound, the activation-mask
+        # kernel at the exact row maximum: the same gradient up to the split's rounding
+        g1, g2 = grad.cpu().numpy(), grad2.cpu().numpy()
+        for l in range(9):
+            sl = slice(256 * l, 256 * l + (256 if l < 8 else 128))
+            assert rel_l2(g1[:, sl], g2[:, sl]) < 1e-5, (l, rel_l2(g1[:, sl], g2[:, sl]))
         check_mask_words(save.cpu(), masks.cpu())
     # oracle in float64 on the points the kernel evaluated (o + d z in fp32, render.py:22 / ray_utils.py:86)
     pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
