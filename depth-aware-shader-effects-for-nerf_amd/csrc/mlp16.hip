@@ -147,7 +147,12 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     }
   }
   if constexpr (SV) {
+#ifdef NERF_SAVE_CONTIG_TIMING   // timing-only A/B build: each quarter's 32 rows as one contiguous 1 KiB
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, rv), sv.rows,
+                                           (int)(sv.loff & 0xFFFu) + 1024 * (4 * T + q), 4 * 32 * sv.hoff, 0);
+#else
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
+#endif
     mask_or(sv, T, bits);
   }
 }
@@ -197,7 +202,11 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     wrows = __builtin_amdgcn_make_buffer_rsrc(save + s0 * kSaveRow, (short)0, 32 * kSaveRow * 4, 0x00020000);
   // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
   // inside the MFMA schedule)
+#ifdef NERF_SAVE_CONTIG_TIMING
+  const uint32_t loff = valid ? ((uint32_t)(lane & 31) * 8 + 4 * h) * 4 : 0x40000000u;
+#else
   const uint32_t loff = valid ? ((uint32_t)(lane & 31) * kSaveRow + 4 * h) * 4 : 0x40000000u;
+#endif
   // training: this wave's mask rows in LDS, zeroed before the quarters OR their bits in
   unsigned* mwave = reinterpret_cast<unsigned*>(lds + kLdsMask) + wave * 32 * kMaskWords;
   unsigned* mrow = mwave + (lane & 31) * kMaskWords + 4 * h;

@@ -1012,7 +1012,12 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
       xs[e] = d * s;
     }
   }
-#ifndef NERF_BW_NO_STORES   // (timing-only A/B build: the cost of the gradient-row stores)
+#if defined(NERF_BW_CONTIG_TIMING)   // timing-only A/B build: each quarter's 32 rows as one contiguous 1 KiB
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
+                                         (int)(((g.loff / 4) % kGradRow) % 8 + 8 * (g.loff / 4 / kGradRow)) * 4 +
+                                             1024 * (4 * T + q),
+                                         4 * 32 * g.slice, 0);
+#elif !defined(NERF_BW_NO_STORES)   // (timing-only A/B build: the cost of the gradient-row stores)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows, (int)g.loff + 4 * (32 * T + 8 * q),
                                          4 * g.slice, 0);
 #endif
@@ -1248,7 +1253,7 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
                         float* grad, hipStream_t s) {
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3) {
-#ifdef NERF_BW_EXACT_MAX   // A/B build: the exact-row-maximum kernel
+#ifndef NERF_BW_BOUND   // the exact-row-maximum kernel (default; NERF_BW_BOUND: the bound-scaled one)
     if (masks)
       hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
@@ -1308,6 +1313,7 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
   const int ka = k0 + (lane & 31), kb = ka + 32;
   const int hm = lane >> 5;
   f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+  double bsum = 0.0;                  // the bias column, in double (one rounding per chunk)
   // uniform trip count for the whole wave (MFMA is a wave-wide instruction); a sample past the
   // chunk end contributes a zero a-operand
   const int pairs = (int)((m1 - m0 + 1) / 2);
@@ -1316,6 +1322,7 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
     const int64_t m = m0 + 2 * p + hm;
     const int64_t mc = m < mlast ? m : mlast;
     const float av = (n < N && m <= mlast) ? a[mc * lda + n] : 0.0f;
+    bsum += (double)av;
     const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? mc : mc / x_div);
     const float x0 = ka < K ? x[xr * ldx + ka] : (ka == K ? 1.0f : 0.0f);
     const float x1 = kb < K ? x[xr * ldx + kb] : (kb == K ? 1.0f : 0.0f);
@@ -1331,6 +1338,10 @@ wgrad_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __res
       if (kb < KP) out[(size_t)row * KP + kb] = acc1[g];
     }
   }
+  // the bias column again from the double sum (the MFMA's f32 value above is overwritten; stores of
+  // one wave land in program order)
+  bsum += __shfl_xor(bsum, 32);
+  if (K >= k0 && K < k0 + 64 && hm == 0 && n < N) out[(size_t)n * KP + K] = (float)bsum;
 }
 
 // The main weight-gradient kernel.  A workgroup computes a (64 WN) x (64 WK) output tile of one

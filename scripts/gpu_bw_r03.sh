@@ -13,7 +13,7 @@ step() {  # name seconds cmd...
   return 0
 }
 step pytest_train 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_autograd.py -q -p no:cacheprovider --timeout 300 --timeout-method thread
-step ab_train 900 bash scripts/ab_train_libs.sh depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_base.so depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_nostore.so
+step ab_train 900 bash scripts/ab_train_libs.sh depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_base.so depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_nostore.so depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_contig.so
 ROOT=$(pwd)
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_train" -o run -- python3 "$ROOT/bench_train.py" --steps 10 --warmup 2 --no-cpu-baseline > "$ROOT/gpurun_out/prof_train.log" 2>&1); echo "prof_train rc=$?"
 
