@@ -14,7 +14,28 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NERFMI_LIB") or os.path.join(_PKG_DIR, "libnerfmi.so")
 
 _c_float_p = ctypes.c_void_p  # device pointers travel as integers
-SAVE_ROW, GRAD_ROW, MASK_ROW = 2400, 2312, 68   # include/nerfmi_train.h NERF_SAVE_ROW, _GRAD_ROW, _MASK_ROW
+SAVE_ROW, GRAD_ROW, MASK_ROW = 2400, 2320, 68   # include/nerfmi_train.h NERF_SAVE_ROW, _GRAD_ROW, _MASK_ROW
+
+
+def tile_rows(M):
+    """Rows a tile-major save/grad buffer of M samples holds (include/nerfmi_train.h NERF_TILE_ROWS):
+    whole 32-sample blocks."""
+    return (M + 31) // 32 * 32
+
+
+def untile(t, M):
+    """A tile-major [tile_rows(M), R] save/grad buffer as the plain [M, R] rows it encodes: element f
+    of sample m sits at (m/32)*32R + (f/8)*256 + (m%32)*8 + f%8 (include/nerfmi_train.h)."""
+    R = t.shape[1]
+    return t.reshape(-1, R // 8, 32, 8).permute(0, 2, 1, 3).reshape(-1, R)[:M]
+
+
+def tile(x):
+    """The inverse of untile: plain [M, R] rows (R % 8 == 0) into a zero-padded tile-major buffer."""
+    M, R = x.shape
+    out = x.new_zeros(tile_rows(M), R)
+    out[:M] = x
+    return out.reshape(-1, 32, R // 8, 8).permute(0, 2, 1, 3).reshape(-1, R).contiguous()
 _V, _I64 = ctypes.c_void_p, ctypes.c_int64
 
 # name -> (restype, argtypes)

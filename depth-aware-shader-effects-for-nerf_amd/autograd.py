@@ -118,7 +118,7 @@ def _param_grads(keys, params, app, rows, save, grad, M, N, packed, need_app, un
 
 def _mlp_backward(packed, packedT, save, masks, sigma, rgb, dsigma, drgb, M):
     lib = _lib.load()
-    grad = torch.empty(M, _lib.GRAD_ROW, device=save.device)
+    grad = torch.empty(_lib.tile_rows(M), _lib.GRAD_ROW, device=save.device)   # tile-major rows
     _lib.check(lib.nerf_mlp_backward(_lib.ptr(packed), _lib.ptr(packedT), _lib.ptr(save), _lib.ptr(masks),
                                      _lib.ptr(sigma), _lib.ptr(rgb), _lib.ptr(dsigma), _lib.ptr(drgb), M,
                                      _lib.ptr(grad), _lib.stream()), "nerf_mlp_backward")
@@ -144,7 +144,7 @@ class _RenderFn(torch.autograd.Function):
         z = torch.empty(B, N, device=dev)
         feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save = torch.empty(M, _lib.SAVE_ROW, device=dev)
+        save = torch.empty(_lib.tile_rows(M), _lib.SAVE_ROW, device=dev)   # tile-major rows
         arith = _lib.get_mlp_arith()
         masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev) if arith == "f16x3" else None
         rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
@@ -204,7 +204,7 @@ class _MLPFn(torch.autograd.Function):
         feat, encd = torch.empty(M, 256, device=dev), torch.empty(M, 32, device=dev)
         z = torch.zeros(M, 1, device=dev)              # one "ray" per point at z = 0: pts = x + d*0 = x
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save = torch.empty(M, _lib.SAVE_ROW, device=dev)
+        save = torch.empty(_lib.tile_rows(M), _lib.SAVE_ROW, device=dev)   # tile-major rows
         arith = _lib.get_mlp_arith()
         masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev) if arith == "f16x3" else None
         if M:

@@ -197,14 +197,35 @@ constexpr int kMaskRow = kMaskRowBytes / 4;                  // 68 words per sam
 // Per-sample gradient row written by the backward pass (nerf_mlp_backward):
 //   [dpre_0 .. dpre_7 (256 each) | dpre_dir (128) | dsigma_pre + pad | dhd (128) | drgb_pre (3) + pad]
 // dpre_l = d loss / d (pre-activation of trunk layer l), dhd = d loss / d hd.  Every slice starts
-// on a 16-byte boundary (the weight-gradient GEMM streams them with 16-byte loads).  dsigma_pre
-// follows dpre_dir: both heads read h7, so their weight gradients run as one 129-row GEMM over
+// on an 8-float boundary (a whole group of the tile-major layout below).  dsigma_pre follows
+// dpre_dir: both heads read h7, so their weight gradients run as one 129-row GEMM over
 // [h7 | enc_d] (param_grads), which reads h7 once.
 constexpr int kGradDir = 8 * kHidden;                        // 2048
 constexpr int kGradSigma = kGradDir + kDirHidden;            // 2176
-constexpr int kGradHd = kGradSigma + 4;                      // 2180
-constexpr int kGradRgb = kGradHd + kDirHidden;               // 2308
-constexpr int kGradRow = kGradRgb + 4;                       // 2312
+constexpr int kGradHd = kGradSigma + 8;                      // 2184
+constexpr int kGradRgb = kGradHd + kDirHidden;               // 2312
+constexpr int kGradRow = kGradRgb + 8;                       // 2320
+
+// Tile-major rows.  The save rows and the gradient rows are stored per block of 32 samples (one
+// wave's), feature groups of 8 outermost: element f of sample m's row (row length R, a multiple
+// of 8) is float
+//     (m / 32) * 32 R  +  (f / 8) * 256  +  (m % 32) * 8  +  f % 8.
+// A kernel's quarter-tile store (4 features of each of a wave's 32 samples, both lane halves) is
+// then one contiguous KiB instead of 32 separate 32-byte pieces of 32 rows: the row-major
+// pieces cost the training forward and the data gradient ~0.3 ms each per 262K-sample launch
+// (same-box A/B, profiles/r03_ab_train_store_variants.log).  Buffers hold tile_rows(M) rows: the
+// last block is whole; its rows past M are zero (the writers clear that block first), so the
+// weight-gradient GEMMs read whole blocks and the padding adds nothing.  A slice starting at
+// feature c (c % 8 == 0) is the same layout at float offset tile_col(c).
+NERF_HD constexpr int64_t tile_rows(int64_t M) { return (M + 31) / 32 * 32; }
+NERF_HD constexpr int64_t tile_col(int c) { return (int64_t)(c / 8) * 256; }
+NERF_HD constexpr int64_t tile_off(int64_t m, int f, int R) {
+  return (m / 32) * 32 * (int64_t)R + (int64_t)(f / 8) * 256 + (m % 32) * 8 + f % 8;
+}
+static_assert(kSaveRow % 8 == 0 && kGradRow % 8 == 0 && kSaveEncX % 8 == 0 && kSaveEncD % 8 == 0 &&
+                  kSaveRDir % 8 == 0 && kSaveHd % 8 == 0 && kGradSigma % 8 == 0 && kGradHd % 8 == 0 &&
+                  kGradRgb % 8 == 0,
+              "every slice of the tile-major rows starts on a feature group");
 
 // Float offset, inside matrix m's fragment array, of element j of lane `lane` in the
 // fragment block (n-tile nt, k-step quad kq): ks = 4*kq + j.

@@ -155,7 +155,8 @@ __device__ __forceinline__ void dense(const float* __restrict__ wmat, const floa
   });
 }
 
-// Training: store ReLU(tile) of an 8-tile activation set into the sample's save row at `off`.
+// Training: store ReLU(tile) of an 8-tile activation set into the sample's save row at `off`
+// (row: the sample's place in its tile-major block, layout.h).
 __device__ __forceinline__ void save_tiles(float* __restrict__ row, int off, const f32x16 (&t8)[8], int ntiles,
                                            int h, bool valid) {
   if (!valid) return;
@@ -167,7 +168,7 @@ __device__ __forceinline__ void save_tiles(float* __restrict__ row, int off, con
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = fmaxf(t8[t][4 * q + e], 0.0f);
-      *reinterpret_cast<f32x4*>(row + off + t * 32 + 8 * q + 4 * h) = v;
+      *reinterpret_cast<f32x4*>(row + tile_col(off + t * 32 + 8 * q) + 4 * h) = v;
     }
   }
 }
@@ -220,17 +221,21 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
 #pragma unroll
   for (int p = 0; p < kPeSteps; ++p) pe_mine[p][lane] = pe[p];
   const bool valid = s0 + (lane & 31) < M;
-  float* srow = SAVE ? save + s * kSaveRow : nullptr;
+  float* srow = SAVE ? save + (s / 32) * 32 * kSaveRow + (s % 32) * 8 : nullptr;   // tile-major (layout.h)
   if constexpr (SAVE) {
     if (valid) {
 #pragma unroll
       for (int p = 0; p < kPeSteps; ++p) {
         const int f = pe_feature(p, h);
-        srow[kSaveEncX + (f < 0 ? kPosEnc : f)] = f < 0 ? 0.0f : pe[p];
+        const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
+        srow[tile_col(F) + F % 8] = f < 0 ? 0.0f : pe[p];
       }
       const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) reinterpret_cast<f32x4*>(srow + kSaveEncD + 16 * h)[q] = ed[q];
+      for (int q = 0; q < 4; ++q) {
+        const int F = kSaveEncD + 16 * h + 4 * q;
+        *reinterpret_cast<f32x4*>(srow + tile_col(F) + F % 8) = ed[q];
+      }
     }
   }
 
@@ -305,7 +310,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(A[t][4 * q + e], 0.0f) + app[4 * q + e];
-          *reinterpret_cast<f32x4*>(srow + kSaveHd + t * 32 + 8 * q + 4 * h) = v;
+          *reinterpret_cast<f32x4*>(srow + tile_col(kSaveHd + t * 32 + 8 * q) + 4 * h) = v;
         }
       }
     }
@@ -343,6 +348,9 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
     return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s, save, encd, masks);
   constexpr int per_block = 32 * NERF_MLP_WAVES;
   const int64_t blocks = (M + per_block - 1) / per_block;
+  // tile-major save rows: the last block's rows past M are zeros (layout.h)
+  if (save && M % 32 && hipMemsetAsync(save + (M / 32) * 32 * kSaveRow, 0, (size_t)32 * kSaveRow * 4, s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "mlp training forward: hipMemsetAsync failed");
   if (save)
     hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M, N,
                        feat, rgb, sigma, out_slot, out_T, save, encd);

@@ -87,7 +87,7 @@ struct QuarterVec {
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 struct SaveAt {      // training forward: where a layer's activations go (see convert4)
   __amdgpu_buffer_rsrc_t rows;   // the wave's 32 activation rows
-  uint32_t loff;                 // this lane's byte offset in them: ((lane & 31) * kSaveRow + 4h) * 4
+  uint32_t loff;                 // this lane's byte offset in the wave's tile-major block: ((lane & 31) 8 + 4h) 4
   int hoff;                      // the layer's slice (floats), uniform
   bool valid;
   unsigned* mrow;                // this lane's mask words in LDS: the sample's row + 4h (words)
@@ -102,8 +102,11 @@ __device__ __forceinline__ void mask_or(const SaveAt& sv, int T, uint32_t bits) 
 }
 // 16 bytes at byte offset voff + 4 * (hoff + c) of the wave's rows: a buffer store, so the lane's
 // address stays one VGPR (the uniform slice goes in soffset, the constant in the offset field).
+// (tile-major rows, layout.h: feature group c / 8 of the slice at hoff; c and hoff multiples of 8, so
+// one store instruction writes the wave's 32 samples x 8 features, 1 KiB, contiguously)
 __device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sv.rows, (int)sv.loff + 4 * c, 4 * sv.hoff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sv.rows, (int)sv.loff + 4 * (int)tile_col(c),
+                                         4 * (int)tile_col(sv.hoff), 0);
 }
 template <int T0, int QG, bool SIGMA>
 __device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {
@@ -147,12 +150,7 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     }
   }
   if constexpr (SV) {
-#ifdef NERF_SAVE_CONTIG_TIMING   // timing-only A/B build: each quarter's 32 rows as one contiguous 1 KiB
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, rv), sv.rows,
-                                           (int)(sv.loff & 0xFFFu) + 1024 * (4 * T + q), 4 * 32 * sv.hoff, 0);
-#else
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
-#endif
     mask_or(sv, T, bits);
   }
 }
@@ -202,11 +200,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     wrows = __builtin_amdgcn_make_buffer_rsrc(save + s0 * kSaveRow, (short)0, 32 * kSaveRow * 4, 0x00020000);
   // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
   // inside the MFMA schedule)
-#ifdef NERF_SAVE_CONTIG_TIMING
   const uint32_t loff = valid ? ((uint32_t)(lane & 31) * 8 + 4 * h) * 4 : 0x40000000u;
-#else
-  const uint32_t loff = valid ? ((uint32_t)(lane & 31) * kSaveRow + 4 * h) * 4 : 0x40000000u;
-#endif
   // training: this wave's mask rows in LDS, zeroed before the quarters OR their bits in
   unsigned* mwave = reinterpret_cast<unsigned*>(lds + kLdsMask) + wave * 32 * kMaskWords;
   unsigned* mrow = mwave + (lane & 31) * kMaskWords + 4 * h;
@@ -499,13 +493,18 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
       for (int p = 0; p < kPeSteps; ++p) {
         const int f = pe_feature(p, h);
+        const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? 0.0f : pe_mine[p * 64 + lane]), wrows,
-                                              (int)loff - 16 * h + 4 * (kSaveEncX + (f < 0 ? kPosEnc : f)), 0, 0);
+                                              (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
       }
       const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        save_store(SaveAt{wrows, loff, 0, true}, 12 * h + kSaveEncD + 4 * q, ed[q]);
+      {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
+        const int F = kSaveEncD + 16 * h + 4 * q;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
+                                               (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+      }
     }
   }
   if (h == 0 && valid) {
@@ -525,6 +524,9 @@ int launch_mlp16(const float* packed, const float* o, const float* d, const floa
   constexpr int per_block = 32 * kW16Waves;
   const int64_t blocks = (M + per_block - 1) / per_block;
   if (save && !masks) return set_error(NERF_ERR_BAD_ARG, "mlp16 training forward: mask rows required");
+  // tile-major save rows: the last block's rows past M are zeros (layout.h), its tail lanes store nothing
+  if (save && M % 32 && hipMemsetAsync(save + (M / 32) * 32 * kSaveRow, 0, (size_t)32 * kSaveRow * 4, s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "mlp16 training forward: hipMemsetAsync failed");
   if (save)
     hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
                        feat, rgb, sigma, out_slot, out_T, save, encd, masks);

@@ -437,17 +437,26 @@ struct GradRows {
   uint32_t loff;   // this lane's byte offset: row (lane & 31), lane half h
 };
 
+// (tile-major rows, layout.h: the wave's block of 32 samples; a lane's 4 features of a group at
+// ((lane & 31) 8 + 4h) floats; a lane past M, or a wave past M, stores nothing)
 __device__ __forceinline__ GradRows grad_rows(float* grad, int64_t s0, int64_t M, int lane) {
-  const int64_t rows = M - s0 < 32 ? M - s0 : 32;
+  const bool any = s0 < M;
   GradRows g;
-  g.res = __builtin_amdgcn_make_buffer_rsrc(grad + s0 * kGradRow, (short)0, (int)(rows * kGradRow * 4), 0x00020000);
-  g.loff = (uint32_t)(lane & 31) * (kGradRow * 4) + 16u * (uint32_t)(lane >> 5);
+  g.res = __builtin_amdgcn_make_buffer_rsrc(grad + (any ? s0 : 0) * kGradRow, (short)0, any ? 32 * kGradRow * 4 : 0,
+                                            0x00020000);
+  g.loff = s0 + (lane & 31) < M ? ((uint32_t)(lane & 31) * 8 + 4 * (uint32_t)(lane >> 5)) * 4 : 0x40000000u;
   return g;
 }
 
-// 16 bytes at float offset off (+ 4 h) of this lane's gradient row
+// Sample s's place in its tile-major block: element f of the row at tile_row(...) + tile_col(f) + f % 8.
+template <typename T>
+__device__ __forceinline__ T* tile_row(T* base, int64_t s, int R) {
+  return base + (s / 32) * 32 * (int64_t)R + (s % 32) * 8;
+}
+
+// 16 bytes at feature off (+ 4 h) of this lane's gradient row (off a multiple of 8)
 __device__ __forceinline__ void grad_store4(const GradRows& g, int off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), g.res, (int)g.loff, 4 * off, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), g.res, (int)g.loff, 4 * (int)tile_col(off), 0);
 }
 
 // d pre-activation = d activation * [activation > 0] (ReLU backward; the saved activation is
@@ -459,7 +468,7 @@ __device__ __forceinline__ void relu_back_store(f32x16 (&x)[8], int ntiles, cons
     if (t >= ntiles) break;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(srow + save_off + t * 32 + 8 * q + 4 * h);
+      const f32x4 a = *reinterpret_cast<const f32x4*>(srow + tile_col(save_off + t * 32 + 8 * q) + 4 * h);
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -483,8 +492,8 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const bool valid = s0 + (lane & 31) < M;
-  const float* srow = save + s * kSaveRow;
-  float* grow = grad + s * kGradRow;
+  const float* srow = tile_row(save, s, kSaveRow);
+  float* grow = tile_row(grad, s, kGradRow);
   const GradRows gr = grad_rows(grad, s0, M, lane);
 
   // rgb head: rgb = sigmoid(v) -> dv = drgb * rgb (1 - rgb) (models.py:159-160)
@@ -497,9 +506,9 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
   // density head: sigma = ReLU(v_s) -> d v_s = dsigma * [sigma > 0]
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
-    grow[kGradSigma] = dsp;
+    grow[tile_col(kGradSigma)] = dsp;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+    for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
   f32x16 A[8], B[8];
   // d hd = W_rgb^T dv (128, accumulator layout in A[0..3])
@@ -627,7 +636,7 @@ __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const
 #pragma unroll
     for (int u = 0; u < CPS; ++u) {
       const int c = st * CPS + u;
-      pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 32 * (c / 4) + 8 * (c % 4));
+      pf[c % RS] = *reinterpret_cast<const f32x4*>(act + 256 * c);   // tile-major: feature group c
     }
     if constexpr (ks == 0) {
 #pragma unroll
@@ -693,8 +702,8 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const bool valid = s0 + (lane & 31) < M;
-  const float* srow = save + s * kSaveRow;
-  float* grow = grad + s * kGradRow;
+  const float* srow = tile_row(save, s, kSaveRow);
+  float* grow = tile_row(grad, s, kGradRow);
   const GradRows gr = grad_rows(grad, s0, M, lane);
   const uint32_t* t16 = reinterpret_cast<const uint32_t*>(packedT);
   const float* invw = packedT + kOffT16Consts + 8;
@@ -708,9 +717,9 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   }
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
-    grow[kGradSigma] = dsp;
+    grow[tile_col(kGradSigma)] = dsp;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+    for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
   f32x16 X[8];
   h16x8 bh[16], bl[16];
@@ -732,7 +741,7 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   uint32_t mask[4];
   relu_back_store(X, 4, srow, kSaveRDir, gr, kGradDir, h);
   float inv_g = split_rows<4>(X, bh, bl);
-  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + save_h(7) + 4 * h, mask, lane);
+  dgrad16<kDirHidden / 16>(t16 + t16_offset(7), bh, bl, X, invw[7], inv_g, srow + tile_col(save_h(7)) + 4 * h, mask, lane);
   const float* wsg = packed + kOffSigmaW;
 #pragma unroll
   for (int t = 0; t < 8; ++t)
@@ -746,7 +755,7 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   for (int l = 7; l >= 1; --l) {
     relu_mask_store(X, mask, gr, l * kHidden);
     inv_g = split_rows<8>(X, bh, bl);
-    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + save_h(l - 1) + 4 * h, mask,
+    dgrad16<kHidden / 16>(t16 + t16_offset(l - 1), bh, bl, X, invw[l - 1], inv_g, srow + tile_col(save_h(l - 1)) + 4 * h, mask,
                           lane);
   }
   relu_mask_store(X, mask, gr, 0);
@@ -882,8 +891,8 @@ mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restr
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
   const bool valid = s0 + (lane & 31) < M;
-  float* grow = grad + s * kGradRow;
-  const GradRows gr = grad_rows(grad, s0 < M ? s0 : M, M, lane);
+  float* grow = tile_row(grad, s, kGradRow);
+  const GradRows gr = grad_rows(grad, s0, M, lane);
   const float* invw = packedT + kOffT16Consts + 8;
 
   // heads, as mlp_backward_kernel
@@ -895,9 +904,9 @@ mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restr
   }
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
-    grow[kGradSigma] = dsp;
+    grow[tile_col(kGradSigma)] = dsp;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+    for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
   f32x16 X[8];
   h16x8 bh[16], bl[16];
@@ -975,7 +984,7 @@ constexpr int kBoLdsFloats = kBoLdsConsts + kT16Consts;               // 99.6 Ki
 
 struct GradAt {                      // where a layer's d pre-activations go, and its mask
   __amdgpu_buffer_rsrc_t rows;       // the wave's gradient rows (tail rows outside: stores dropped)
-  uint32_t loff;                     // this lane's byte offset: ((lane & 31) kGradRow + 4h) 4
+  uint32_t loff;                     // this lane's byte offset in the tile-major block: ((lane & 31) 8 + 4h) 4
   int slice;                         // the layer's first float in the row, uniform
   const uint32_t* mrow;              // this lane's mask words in LDS (sample row + 4h words)
   int mlay;                          // the layer's words in the row: 8 * layer, uniform
@@ -1012,14 +1021,9 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
       xs[e] = d * s;
     }
   }
-#if defined(NERF_BW_CONTIG_TIMING)   // timing-only A/B build: each quarter's 32 rows as one contiguous 1 KiB
+#ifndef NERF_BW_NO_STORES   // (timing-only A/B build: the cost of the gradient-row stores)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
-                                         (int)(((g.loff / 4) % kGradRow) % 8 + 8 * (g.loff / 4 / kGradRow)) * 4 +
-                                             1024 * (4 * T + q),
-                                         4 * 32 * g.slice, 0);
-#elif !defined(NERF_BW_NO_STORES)   // (timing-only A/B build: the cost of the gradient-row stores)
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows, (int)g.loff + 4 * (32 * T + 8 * q),
-                                         4 * g.slice, 0);
+                                         (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice), 0);
 #endif
   if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
     Operand& op = in[OP0 + QG / 2];
@@ -1057,11 +1061,10 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
   // store nothing
   const bool valid = s0 + (lane & 31) < M;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
-  const int64_t rows_here = s0 < M ? imin64(M - s0, 32) : 0;
-  GradAt ga;
-  ga.rows = __builtin_amdgcn_make_buffer_rsrc(grad + imin64(s0, M) * kGradRow, (short)0, (int)(rows_here * kGradRow * 4),
-                                              0x00020000);
-  ga.loff = valid ? ((uint32_t)(lane & 31) * kGradRow + 4 * h) * 4 : 0x40000000u;
+  GradAt ga;                          // the wave's tile-major block (layout.h)
+  ga.rows = __builtin_amdgcn_make_buffer_rsrc(grad + (s0 < M ? s0 : 0) * kGradRow, (short)0,
+                                              s0 < M ? 32 * kGradRow * 4 : 0, 0x00020000);
+  ga.loff = valid ? ((uint32_t)(lane & 31) * 8 + 4 * h) * 4 : 0x40000000u;
   // the wave's 32 mask rows (8,704 contiguous bytes) into LDS; constants and w_sigma
   uint32_t* mwave = reinterpret_cast<uint32_t*>(lds + kBoLdsMask) + wave * 32 * kMaskRow;
   for (int i = lane; i < 32 * kMaskRow / 4; i += 64) {
@@ -1098,11 +1101,11 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
   __syncthreads();                    // mask rows, w_sigma and constants in LDS
   const float* cst = lds + kBoLdsConsts;
   const float* wsig = lds + kBoLdsWsig;
-  float* grow = grad + s * kGradRow;
+  float* grow = tile_row(grad, s, kGradRow);
   if (valid && h == 0) {
-    grow[kGradSigma] = dsp;
+    grow[tile_col(kGradSigma)] = dsp;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) grow[kGradRgb + c] = dv[c];
+    for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
   // d hd rows; d pre_dir = d hd [r_dir > 0] (hd = ReLU(dir pre) + appearance): rows, max, split at
   // the exact maximum into operands 8..15 (the dir layer's 8 k-steps)
@@ -1123,10 +1126,10 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
           dhd[t][4 * q + e] = b[e];
           m_dir = fmaxf(m_dir, fabsf(b[e]));
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows,
-                                               (int)ga.loff + 4 * (kGradHd + 32 * t + 8 * q), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), ga.rows,
-                                               (int)ga.loff + 4 * (kGradDir + 32 * t + 8 * q), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows, (int)ga.loff,
+                                               4 * (int)tile_col(kGradHd + 32 * t + 8 * q), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), ga.rows, (int)ga.loff,
+                                               4 * (int)tile_col(kGradDir + 32 * t + 8 * q), 0);
       }
   }
   m_dir = sample_max(m_dir);
@@ -1252,6 +1255,9 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
                         const float* sigma, const float* rgb, const float* dsigma, const float* drgb, int64_t M,
                         float* grad, hipStream_t s) {
   if (M == 0) return NERF_OK;
+  // tile-major gradient rows: the last block's rows past M are zeros (layout.h); its tail lanes store nothing
+  if (M % 32 && hipMemsetAsync(grad + (M / 32) * 32 * kGradRow, 0, (size_t)32 * kGradRow * 4, s) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "mlp backward: hipMemsetAsync failed");
   if (g_mlp_arith == NERF_ARITH_F16X3) {
 #ifndef NERF_BW_BOUND   // the exact-row-maximum kernel (default; NERF_BW_BOUND: the bound-scaled one)
     if (masks)
@@ -1367,7 +1373,8 @@ __device__ __forceinline__ f32x4 load4_masked(const float* __restrict__ p, int v
   return v;
 }
 
-template <int WN, int WK>
+// BLK: a (and x when x_div == 1) in the tile-major row layout (layout.h), lda / ldx their row lengths.
+template <int WN, int WK, bool BLK>
 __global__ void __launch_bounds__(256, 2)
 wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
                  int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
@@ -1401,13 +1408,15 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
     sfor<WN>([&](auto pc) __attribute__((always_inline)) {
       constexpr int p = decltype(pc)::value;
       const int64_t m = mb + a_r + AROWS * p;
-      ra[p] = (m < m1 && a_valid > 0) ? load4_masked(a + m * lda + n0 + a_c, a_valid) : zero4;
+      const float* ap = BLK ? a + tile_off(m, n0 + a_c, (int)lda) : a + m * lda + n0 + a_c;
+      ra[p] = (m < m1 && a_valid > 0) ? load4_masked(ap, a_valid) : zero4;
     });
     sfor<WK>([&](auto pc) __attribute__((always_inline)) {
       constexpr int p = decltype(pc)::value;
       const int64_t m = mb + x_r + XROWS * p;
       const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? m : m / x_div);
-      rx[p] = (m < m1 && x_valid > 0) ? load4_masked(x + xr * ldx + k0 + x_c, x_valid) : zero4;
+      const float* xp = (BLK && x_div == 1) ? x + tile_off(m, k0 + x_c, (int)ldx) : x + xr * ldx + k0 + x_c;
+      rx[p] = (m < m1 && x_valid > 0) ? load4_masked(xp, x_valid) : zero4;
     });
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
@@ -1502,7 +1511,11 @@ __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
 // XD1 (x_div == 1, one x row per sample: every trunk/head layer): the loader's per-sample offsets
 // are stage-invariant VGPRs and only the buffer descriptors move per stage (no VALU address work;
 // the generic x path divides and carries per sample, ~130 VALU per stage).
-template <int WN, int WK, bool XD1>
+// BLK: a (and x when XD1) tile-major (layout.h): a stage of 16 samples lies in one 32-sample block,
+// the stage's resource is based at its first sample's place in that block, a sample j of a slot at
+// +32 j bytes; past the chunk end only the sentinel stage (an empty resource) and the zero padding
+// of the last block are read.
+template <int WN, int WK, bool XD1, bool BLK>
 __global__ void __launch_bounds__(256, WN == 4 ? 1 : 2)   // 256 x 64 tiles: 94 KB of LDS, one block per CU
 wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
                 int64_t x_div, int64_t M, int ntk, int tiles, int chunks, int clen, float* __restrict__ partial) {
@@ -1541,7 +1554,10 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
 #pragma unroll
   for (int q = 0; q < SA; ++q) {
     const int slot = tid + 256 * q, col = slot % BN, oct = slot / BN;
-    aoff[q] = (slot < 2 * BN && n0 + col < N) ? (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)(n0 + col) : kOut;
+    const int nc = n0 + col;
+    aoff[q] = (slot < 2 * BN && nc < N)
+                  ? (BLK ? 4u * (uint32_t)(tile_col(nc) + nc % 8 + 64 * oct) : (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)nc)
+                  : kOut;
   }
 #pragma unroll
   for (int q = 0; q < SX; ++q) {
@@ -1552,14 +1568,16 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
 #pragma unroll
   for (int q = 0; q < SA; ++q)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) avo[q][j] = aoff[q] == kOut ? kOut : aoff[q] + (uint32_t)j * lda4;
+    for (int j = 0; j < 8; ++j) avo[q][j] = aoff[q] == kOut ? kOut : aoff[q] + (uint32_t)j * (BLK ? 32u : lda4);
   if constexpr (XD1) {
 #pragma unroll
     for (int q = 0; q < SX; ++q) {
       const int oct = (tid + 256 * q) / BK;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        xvo[q][j] = xcol[q] == kOut ? kOut : (uint32_t)(8 * oct + j) * ldx4 + xcol[q];
+        xvo[q][j] = xcol[q] == kOut ? kOut
+                    : BLK ? 4u * (uint32_t)(tile_col(xcol[q] / 4) + (xcol[q] / 4) % 8 + 8 * (8 * oct + j))
+                          : (uint32_t)(8 * oct + j) * ldx4 + xcol[q];
     }
   }
   const uint32_t xd = x_div == 0 ? 0xFFFFFFFFu : (uint32_t)x_div;
@@ -1573,8 +1591,11 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage);
+    const int64_t ms = m0 + rel0;             // BLK: the stage's place in its block; empty past the chunk
+    const bool live = rel0 < mrel_end;
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
 #pragma unroll
     for (int q = 0; q < SA; ++q)
 #pragma unroll
@@ -1582,7 +1603,8 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
         ra[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[q][j], 0, 0));
     if constexpr (XD1) {
       const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+          const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+          BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
       for (int q = 0; q < SX; ++q)
 #pragma unroll
@@ -1743,6 +1765,7 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf1
     p2[j] = (__bf16)r2;
   }
 }
+template <bool BLK>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
 __global__ void __launch_bounds__(512, 1)
 wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
                    int clen, float* __restrict__ partial) {
@@ -1758,28 +1781,36 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   // of the octet at voffset avo + soffset j * lda4 (wave-uniform)
   const int col = tid % kWT, oct = tid / kWT;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const uint32_t avo = (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)col;
+  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(col) + col % 8 + 64 * oct) : (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)col;
+  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
   uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
 #pragma unroll
-  for (int t = 0; t < 2; ++t) xvo[t] = (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)(64 * wk + 32 * t + c);
+  for (int t = 0; t < 2; ++t) {
+    const int xc = 64 * wk + 32 * t + c;
+    xvo[t] = BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)xc;
+  }
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
   float ra[2][8], rx[2][2][8];   // two stages in flight: stage k's values in set k % 2
   double bacc = 0.0;                 // bias column in double: one rounding per chunk
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * lda4), 0));
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * ldx4), 0));
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0));
   };
   auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
@@ -1864,6 +1895,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
 // registers, so two workgroups share a CU and keep more loads in flight (1 KiB of a + 252 B of x
 // per sample).  Loads run two stages ahead, unconditionally.  75 us per 262K-sample launch against
 // 105 us on 256 x 64 tiles of wgrad_bf_kernel (scripts/wgrad_libs_trace.sh, K=63).
+template <bool BLK>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
 __global__ void __launch_bounds__(512)
 wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int K,
                     int64_t M, int clen, float* __restrict__ partial) {
@@ -1874,26 +1906,33 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const uint32_t avo = (uint32_t)(8 * h) * lda4 + 4u * (uint32_t)(32 * w + c);
+  const int ac = 32 * w + c;
+  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h) : (uint32_t)(8 * h) * lda4 + 4u * (uint32_t)ac;
+  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
   // x loader: column tid % 64 (past K: an offset beyond any resource, reads 0), samples 2p, 2p+1
   const int xc = tid & 63, xp = tid >> 6;
-  const uint32_t xvo = xc < K ? (uint32_t)(2 * xp) * ldx4 + 4u * (uint32_t)xc : 0x80000000u;
+  const uint32_t xvo = xc < K ? (BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 16 * xp) : (uint32_t)(2 * xp) * ldx4 + 4u * (uint32_t)xc)
+                              : 0x80000000u;
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
   float ra[2][8], rx[2][2];
   double bacc = 0.0;                 // bias column in double: one rounding per chunk
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
     const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;
     const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (m0 + rel0) * lda), (short)0, (int)((mrel_end - rel0) * lda4), 0x00020000);
+        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
     const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (m0 + rel0) * ldx), (short)0, (int)((mrel_end - rel0) * ldx4), 0x00020000);
+        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * lda4), 0));
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * ldx4), 0));
+      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * xs4), 0));
   };
   auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
@@ -1969,18 +2008,18 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   if (h == 0) out[(size_t)(32 * w + c) * KP + K] = (float)bacc;
 }
 
-template <int WN, int WK>
+template <int WN, int WK, bool BLK>
 static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
                            int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
   if (x_div == 1)
-    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, true>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K,
-                       x_div, M, ntk, tiles, chunks, clen, ws);
+    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, true, BLK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x,
+                       ldx, K, x_div, M, ntk, tiles, chunks, clen, ws);
   else
-    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, false>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx,
-                       K, x_div, M, ntk, tiles, chunks, clen, ws);
+    hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, false, BLK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x,
+                       ldx, K, x_div, M, ntk, tiles, chunks, clen, ws);
   return check_launch("wgrad_bf_kernel");
 }
 
@@ -2045,42 +2084,61 @@ size_t wgrad_workspace_floats(int64_t M, int N, int K) {
   return (size_t)chunks * wgrad_stride(N, K);
 }
 
-template <int WN, int WK>
+template <int WN, int WK, bool BLK>
 static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
                             int64_t M, int chunks, float* ws, hipStream_t s) {
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
-  hipLaunchKernelGGL((wgrad_lds_kernel<WN, WK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K, x_div,
-                     M, ntk, tiles, chunks, ws);
+  hipLaunchKernelGGL((wgrad_lds_kernel<WN, WK, BLK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K,
+                     x_div, M, ntk, tiles, chunks, ws);
   return check_launch("wgrad_lds_kernel");
 }
 
+// tiled: a (and x when x_div == 1) are tile-major rows (layout.h) of row length lda / ldx, each
+// pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
-                 const WgradSplit* split = nullptr) {
+                 const WgradSplit* split = nullptr, bool tiled = false) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
+  if (tiled && !(aligned && lda % 8 == 0 && (x_div != 1 || ldx % 8 == 0)))
+    return set_error(NERF_ERR_BAD_ARG, "wgrad: tile-major operands must be aligned with row lengths % 8 == 0");
   int rc;
   // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K);
     chunks = (int)((M + clen - 1) / clen);
     if (wgrad_whole_tile(N, K) && x_div == 1) {
-      hipLaunchKernelGGL(wgrad_bf256_kernel, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
+      if (tiled)
+        hipLaunchKernelGGL(wgrad_bf256_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
+      else
+        hipLaunchKernelGGL(wgrad_bf256_kernel<false>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
       rc = check_launch("wgrad_bf256_kernel");
     } else if (N == kWT && K <= 64 && x_div == 1) {
-      hipLaunchKernelGGL(wgrad_bf_k64_kernel, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M, clen, ws);
+      if (tiled)
+        hipLaunchKernelGGL(wgrad_bf_k64_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M,
+                           clen, ws);
+      else
+        hipLaunchKernelGGL(wgrad_bf_k64_kernel<false>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M,
+                           clen, ws);
       rc = check_launch("wgrad_bf_k64_kernel");
-    } else if (K <= 64 && N > 64) rc = launch_wgrad_bf<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
-    else rc = launch_wgrad_bf<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
-  } else if (aligned && K >= 1 && K <= 64 && N > 64)
-    rc = launch_wgrad_lds<4, 1>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
-  else if (aligned && K >= 1)
-    rc = launch_wgrad_lds<2, 2>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
-  else {
+    } else if (K <= 64 && N > 64) {
+      rc = tiled ? launch_wgrad_bf<4, 1, true>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s)
+                 : launch_wgrad_bf<4, 1, false>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+    } else {
+      rc = tiled ? launch_wgrad_bf<2, 2, true>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s)
+                 : launch_wgrad_bf<2, 2, false>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+    }
+  } else if (aligned && K >= 1 && K <= 64 && N > 64) {
+    rc = tiled ? launch_wgrad_lds<4, 1, true>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s)
+               : launch_wgrad_lds<4, 1, false>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+  } else if (aligned && K >= 1) {
+    rc = tiled ? launch_wgrad_lds<2, 2, true>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s)
+               : launch_wgrad_lds<2, 2, false>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+  } else {
     const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N,
                        x, ldx, K, x_div, M, ws);
@@ -2099,13 +2157,16 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
 // [r*group, (r+1)*group) with stride ld: per-ray rows pass the gradient rows (group = N); a single
 // broadcast row passes the already-reduced bias gradient of appearance_projection (group = 1).
 __global__ void __launch_bounds__(128)
-app_grad_kernel(const float* __restrict__ src, int64_t ld, int group, const float* __restrict__ packed,
+app_grad_kernel(const float* __restrict__ src, int64_t ld, int group, int tiled, const float* __restrict__ packed,
                 float* __restrict__ dapp) {
   __shared__ float sum[kDirHidden];
   const int64_t r = blockIdx.x;
   const int n = threadIdx.x;
   double acc = 0.0;
-  for (int s = 0; s < group; ++s) acc += (double)src[(r * group + s) * ld + n];
+  for (int s = 0; s < group; ++s) {
+    const int64_t m = r * group + s;     // tiled: gradient rows (layout.h), src at the slice's tile_col
+    acc += (double)src[tiled ? tile_off(m, n, (int)ld) : m * ld + n];
+  }
   sum[n] = (float)acc;
   __syncthreads();
   if (n < kAppDim) {
@@ -2117,9 +2178,9 @@ app_grad_kernel(const float* __restrict__ src, int64_t ld, int group, const floa
 }
 
 int launch_app_grad(const float* src, int64_t ld, int64_t rows, int group, const float* packed, float* dapp,
-                    hipStream_t s) {
+                    hipStream_t s, bool tiled) {
   if (rows == 0) return NERF_OK;
-  hipLaunchKernelGGL(app_grad_kernel, dim3((unsigned)rows), dim3(128), 0, s, src, ld, group, packed, dapp);
+  hipLaunchKernelGGL(app_grad_kernel, dim3((unsigned)rows), dim3(128), 0, s, src, ld, group, (int)tiled, packed, dapp);
   return check_launch("app_grad_kernel");
 }
 
@@ -2208,9 +2269,9 @@ static int forward_arith(const void* ws) {
 }
 
 static size_t train_carve(int64_t B, int N, size_t* off) {
-  const size_t b = (size_t)B, M = b * (size_t)N;
+  const size_t b = (size_t)B, M = b * (size_t)N, MT = (size_t)tile_rows((int64_t)M);   // tile-major rows (layout.h)
   const size_t sizes[T_COUNT] = {b * 3, b * N, b * kRayFeat, b * 32, M * 3, M, b * 4, M, M * 3, b,
-                                 M * kSaveRow, M * kMaskRow, M * kGradRow, max_wgrad_floats((int64_t)M)};
+                                 MT * kSaveRow, M * kMaskRow, MT * kGradRow, max_wgrad_floats((int64_t)M)};
   size_t at = 0;
   for (int i = 0; i < T_COUNT; ++i) {
     off[i] = at;
@@ -2322,26 +2383,28 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   // gradient with the first column block only.  The skip layer's [h3 | enc_x] runs as a 256 x 256
   // block (the whole-tile kernel) plus the 63 PE columns, instead of one 256 x 319 GEMM on 128 x 128
   // tiles (416 -> ~300 us per step).
-  struct Job { const float* a; int n; const float* x; int K; int p; int k0; int ldo; bool bias; };
+  // save and grad are tile-major rows (layout.h): a slice starting at feature c is the same layout at
+  // float offset tile_col(c)
+  struct Job { int a; int n; int x; int K; int p; int k0; int ldo; bool bias; };
   constexpr int kSkipK = kHidden + kPosEnc;
   const Job jobs[] = {
-      {grad + 0, kHidden, save + kSaveEncX, kPosEnc, 0, 0, kPosEnc, true},
-      {grad + 1 * kHidden, kHidden, save + save_h(0), kHidden, 2, 0, kHidden, true},
-      {grad + 2 * kHidden, kHidden, save + save_h(1), kHidden, 4, 0, kHidden, true},
-      {grad + 3 * kHidden, kHidden, save + save_h(2), kHidden, 6, 0, kHidden, true},
-      {grad + 4 * kHidden, kHidden, save + save_h(3), kHidden, 8, 0, kSkipK, true},                  // h3 ..
-      {grad + 4 * kHidden, kHidden, save + save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false},  // .. | enc_x
-      {grad + 5 * kHidden, kHidden, save + save_h(4), kHidden, 10, 0, kHidden, true},
-      {grad + 6 * kHidden, kHidden, save + save_h(5), kHidden, 12, 0, kHidden, true},
-      {grad + 7 * kHidden, kHidden, save + save_h(6), kHidden, 14, 0, kHidden, true},
-      {grad + kGradRgb, 3, save + kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true},
+      {0, kHidden, kSaveEncX, kPosEnc, 0, 0, kPosEnc, true},
+      {1 * kHidden, kHidden, save_h(0), kHidden, 2, 0, kHidden, true},
+      {2 * kHidden, kHidden, save_h(1), kHidden, 4, 0, kHidden, true},
+      {3 * kHidden, kHidden, save_h(2), kHidden, 6, 0, kHidden, true},
+      {4 * kHidden, kHidden, save_h(3), kHidden, 8, 0, kSkipK, true},                  // h3 ..
+      {4 * kHidden, kHidden, save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false},  // .. | enc_x
+      {5 * kHidden, kHidden, save_h(4), kHidden, 10, 0, kHidden, true},
+      {6 * kHidden, kHidden, save_h(5), kHidden, 12, 0, kHidden, true},
+      {7 * kHidden, kHidden, save_h(6), kHidden, 14, 0, kHidden, true},
+      {kGradRgb, 3, kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true},
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
   for (const Job& j : jobs) {
     if (wgrad_workspace_floats(M, j.n, j.K) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
-    if ((rc = launch_wgrad(j.a, kGradRow, j.n, j.x, kSaveRow, j.K, 1, M, g[j.p] + j.k0, j.ldo, j.bias ? g[j.p + 1] : nullptr,
-                           0, ws, s)))
+    if ((rc = launch_wgrad(grad + tile_col(j.a), kGradRow, j.n, save + tile_col(j.x), kSaveRow, j.K, 1, M, g[j.p] + j.k0,
+                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, ws, s, nullptr, true)))
       return rc;
   }
   // dir_linear (128 rows over [h7 | enc_d]) and the density head (1 row over h7) in one GEMM: the
@@ -2351,20 +2414,20 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   if (wgrad_workspace_floats(M, kDirHidden + 1, kHidden + kDirEnc) > ws_floats)
     return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
   const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B]};
-  if ((rc = launch_wgrad(grad + kGradDir, kGradRow, kDirHidden + 1, save + save_h(7), kSaveRow, kHidden + kDirEnc, 1, M,
-                         g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads)))
+  if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirHidden + 1, save + tile_col(save_h(7)), kSaveRow,
+                         kHidden + kDirEnc, 1, M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads, true)))
     return rc;
   if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
     return NERF_OK;
   }
-  // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1)
+  // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1; row-major)
   const int64_t xdiv = app_rows == 1 ? 0 : N;
-  if ((rc = launch_wgrad(grad + kGradHd, kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W], kAppDim,
-                         g[P_APP_B], 0, ws, s)))
+  if ((rc = launch_wgrad(grad + tile_col(kGradHd), kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
+                         kAppDim, g[P_APP_B], 0, ws, s, nullptr, true)))
     return rc;
   if (!dapp) return NERF_OK;
-  if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s);
-  return launch_app_grad(grad + kGradHd, kGradRow, app_rows, N, packed, dapp, s);
+  if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s, false);
+  return launch_app_grad(grad + tile_col(kGradHd), kGradRow, app_rows, N, packed, dapp, s, true);
 }
 
 int nerf_param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,

@@ -186,7 +186,8 @@ class Trainer:
         dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
         feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
         rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-        save, grad = torch.empty(M, _lib.SAVE_ROW, device=dev), torch.empty(M, _lib.GRAD_ROW, device=dev)
+        MT = _lib.tile_rows(M)                                       # tile-major save/grad rows
+        save, grad = torch.empty(MT, _lib.SAVE_ROW, device=dev), torch.empty(MT, _lib.GRAD_ROW, device=dev)
         masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev)
         rgb_map, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
         dsig, drgb, sq = torch.empty(M, device=dev), torch.empty(M, 3, device=dev), torch.empty(B, device=dev)

@@ -27,7 +27,11 @@ extern "C" {
 
 /* Per-sample rows the forward saves / the backward writes (floats). */
 #define NERF_SAVE_ROW 2400 /* [h0..h3 | enc_x(64) | h4..h7 | enc_d(32) | r_dir(128) | hd(128)] */
-#define NERF_GRAD_ROW 2312 /* [dpre_0..7 (256 each) | dpre_dir(128) | dsigma+pad | dhd(128) | drgb(3)+pad] */
+#define NERF_GRAD_ROW 2320 /* [dpre_0..7 (256 each) | dpre_dir(128) | dsigma+pad(8) | dhd(128) | drgb(3)+pad(8)] */
+/* Both are stored tile-major: per block of 32 samples, feature groups of 8 outermost.  Element f
+ * of sample m's row (row length R) is float (m/32)*32*R + (f/8)*256 + (m%32)*8 + f%8, and a buffer
+ * of M samples holds NERF_TILE_ROWS(M) rows (the last block whole; its rows past M are zero). */
+#define NERF_TILE_ROWS(M) ((((M) + 31) / 32) * 32)
 /* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):
  * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes (csrc/layout.h kMaskRow). */
 #define NERF_MASK_ROW 68
@@ -62,7 +66,8 @@ int nerf_pack_weights_transposed_host(const float* const* params, float* packedT
 /* nerf_ray_features plus enc_d (R,32): PE_4(d) (models.py:122), zero-padded. */
 int nerf_ray_features_train(const float* packed, const float* dirs, int64_t R, const float* app,
                             int64_t app_rows, float* feat, float* enc_d, nerf_stream_t stream);
-/* nerf_mlp_forward (no scatter) that also writes save (R*N, NERF_SAVE_ROW) and, under the f16x3
+/* nerf_mlp_forward (no scatter) that also writes save (NERF_TILE_ROWS(R*N), NERF_SAVE_ROW,
+ * tile-major, padding rows zeroed) and, under the f16x3
  * arithmetic, masks (R*N, NERF_MASK_ROW) (required there; ignored under f32, may be null). */
 int nerf_mlp_forward_train(const float* packed, const float* origins, const float* dirs,
                            const float* z_vals, int64_t R, int N, const float* ray_feat,
@@ -80,19 +85,20 @@ int nerf_composite_backward(const float* rgb, const float* sigma, const float* z
 int nerf_composite_backward_grad(const float* rgb, const float* sigma, const float* z_vals,
                                  const float* grad_rgb_map, const float* grad_depth_map, int64_t B,
                                  int N, float* dsigma, float* drgb, nerf_stream_t stream);
-/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (M, NERF_GRAD_ROW).  Under
+/* Data gradients of NeRF.forward (models.py:105-162) on MFMA: grad (NERF_TILE_ROWS(M),
+ * NERF_GRAD_ROW, tile-major; save as the forward wrote it).  Under
  * f16x3 the ReLU masks come from `masks` when non-null (an f16x3 forward's), else from the saved
  * activations; the f32 backward always reads the activations. */
 int nerf_mlp_backward(const float* packed, const float* packedT, const float* save,
                       const uint32_t* masks, const float* sigma, const float* rgb,
                       const float* dsigma, const float* drgb, int64_t M, float* grad,
                       nerf_stream_t stream);
-/* Every parameter gradient (+ appearance rows) from save and grad rows. */
+/* Every parameter gradient (+ appearance rows) from the tile-major save and grad rows. */
 size_t nerf_param_grads_workspace_bytes(int64_t M);
 int nerf_param_grads(const float* save, const float* grad, int64_t M, int N, const float* app,
                      int64_t app_rows, const float* packed, float* const* param_grads, float* dapp,
                      void* workspace, size_t ws_bytes, nerf_stream_t stream);
-/* out_w[n][k] = sum_m a[m*lda+n] x[(m/x_div)*ldx+k] (x_div 0: row 0), out_b[n] = sum_m a[m*lda+n]
+/* Plain row-major operands: out_w[n][k] = sum_m a[m*lda+n] x[(m/x_div)*ldx+k] (x_div 0: row 0), out_b[n] = sum_m a[m*lda+n]
  * (nullable); accumulate adds to the outputs instead of overwriting. */
 size_t nerf_wgrad_workspace_bytes(int64_t M, int N, int K);
 int nerf_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,

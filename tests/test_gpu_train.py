@@ -161,9 +161,9 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
     a, rows = (None, 0) if app is None else (app.reshape(1, 32).to(dev).contiguous(), 1)
     feat, encd = torch.empty(R, 256, device=dev), torch.empty(R, 32, device=dev)
     rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
-    save = torch.empty(M, L.SAVE_ROW, device=dev)
+    save = torch.empty(L.tile_rows(M), L.SAVE_ROW, device=dev)
     masks = torch.empty(M, L.MASK_ROW, dtype=torch.int32, device=dev)
-    grad = torch.zeros(M, L.GRAD_ROW, device=dev)
+    grad = torch.zeros(L.tile_rows(M), L.GRAD_ROW, device=dev)
     s = L.stream()
     L.check(lib.nerf_ray_features_train(L.ptr(packed), L.ptr(dg), R, L.ptr(a), rows, L.ptr(feat), L.ptr(encd), s),
             "feat")
@@ -181,11 +181,11 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
     if f16:
         # the mask-row kernel splits each layer's gradient at a scale from a bound, the activation-mask
         # kernel at the exact row maximum: the same gradient up to the split's rounding
-        g1, g2 = grad.cpu().numpy(), grad2.cpu().numpy()
+        g1, g2 = L.untile(grad.cpu(), M).numpy(), L.untile(grad2.cpu(), M).numpy()
         for l in range(9):
             sl = slice(256 * l, 256 * l + (256 if l < 8 else 128))
             assert rel_l2(g1[:, sl], g2[:, sl]) < 1e-5, (l, rel_l2(g1[:, sl], g2[:, sl]))
-        check_mask_words(save.cpu(), masks.cpu())
+        check_mask_words(L.untile(save.cpu(), M), masks.cpu())
     # oracle in float64 on the points the kernel evaluated (o + d z in fp32, render.py:22 / ray_utils.py:86)
     pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
     dexp = d[:, None, :].expand(R, N, 3).reshape(-1, 3)
@@ -196,7 +196,8 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
     for t in pres:
         t.retain_grad()
     ((rgb_o * g_rgb.double()).sum() + (sigma_o[:, 0] * g_sigma.double()).sum()).backward()
-    return dict(rgb=rgb.cpu(), sigma=sigma.cpu(), save=save.cpu(), grad=grad.cpu(), encd=encd.cpu(), pts=pts,
+    return dict(rgb=rgb.cpu(), sigma=sigma.cpu(), save=L.untile(save.cpu(), M), grad=L.untile(grad.cpu(), M),
+                save_tiled=save.cpu(), grad_tiled=grad.cpu(), encd=encd.cpu(), pts=pts,
                 dexp=dexp, rgb_o=rgb_o.detach(), sigma_o=sigma_o.detach(), pres=pres, st64=st64)
 
 
@@ -238,7 +239,7 @@ def test_param_grads_match_autograd(ref_state, app_vec, with_app):
     app = app_vec if with_app else None
     R, N = 96, 11
     r = _mlp_forward_backward(ref_state, app, R=R, N=N)
-    save, grad = r["save"].to(dev), r["grad"].to(dev)
+    save, grad = r["save_tiled"].to(dev), r["grad_tiled"].to(dev)
     packed, _, ts = packed_of(ref_state, dev)
     grads = [torch.empty_like(t) for t in ts]
     arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in grads])
