@@ -1259,13 +1259,13 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
   if (M % 32 && hipMemsetAsync(grad + (M / 32) * 32 * kGradRow, 0, (size_t)32 * kGradRow * 4, s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "mlp backward: hipMemsetAsync failed");
   if (g_mlp_arith == NERF_ARITH_F16X3) {
-#ifndef NERF_BW_BOUND   // the exact-row-maximum kernel (default; NERF_BW_BOUND: the bound-scaled one)
+#ifndef NERF_BW_EXACT   // the bound-scaled kernel (default; NERF_BW_EXACT: the exact-row-maximum one, A/B)
     if (masks)
-      hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
+      hipLaunchKernelGGL(mlp_backward16_bound_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
 #else
     if (masks)
-      hipLaunchKernelGGL(mlp_backward16_bound_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
+      hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
 #endif
     else
@@ -1290,12 +1290,19 @@ constexpr int kWChunk = 2048;   // samples per chunk
 // 256 blocks instead of 128.  The 128x128-tile launches hold two blocks per CU; those with fewer
 // than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
 static inline bool wgrad_whole_tile(int N, int K) { return N == 256 && K == 256; }
-static inline int wgrad_chunk_len(int N, int K) {
+static inline int wgrad_chunk_len_big(int N, int K) {
   if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
   if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
                                                     // 3 % faster but doubled the reduction)
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
   return tiles == 1 ? kWChunk / 4 : tiles == 2 ? kWChunk / 2 : kWChunk;
+}
+// Short GEMMs (the per-ray ones over B rows) halve the chunk down to one 16-sample stage until
+// there are >= 256 chunks: 4,096 rays in 1,024-row chunks ran 8 blocks, 80-100 us per launch.
+static inline int wgrad_chunk_len(int N, int K, int64_t M) {
+  int c = wgrad_chunk_len_big(N, K);
+  while (c > 16 && (M + c - 1) / c < 256) c /= 2;
+  return c;
 }
 
 NERF_HD inline int64_t wgrad_stride(int N, int K) { return (((int64_t)N * (K + 1)) + 3) & ~(int64_t)3; }
@@ -1373,11 +1380,12 @@ __device__ __forceinline__ f32x4 load4_masked(const float* __restrict__ p, int v
   return v;
 }
 
-// BLK: a (and x when x_div == 1) in the tile-major row layout (layout.h), lda / ldx their row lengths.
+// BLK: a in the tile-major row layout (layout.h), and x too when xblk (then x_div == 1); lda / ldx their
+// row lengths.
 template <int WN, int WK, bool BLK>
 __global__ void __launch_bounds__(256, 2)
 wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __restrict__ x, int64_t ldx, int K,
-                 int64_t x_div, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
+                 int64_t x_div, int xblk, int64_t M, int ntk, int tiles, int chunks, float* __restrict__ partial) {
   static_assert(WN * WK == 4, "four waves");
   constexpr int BN = 64 * WN, BK = 64 * WK;
   constexpr int APAD = BN + 32, XPAD = BK + 32;    // row s+1 lands 32 banks away from row s
@@ -1415,7 +1423,7 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
       constexpr int p = decltype(pc)::value;
       const int64_t m = mb + x_r + XROWS * p;
       const int64_t xr = x_div == 0 ? 0 : (x_div == 1 ? m : m / x_div);
-      const float* xp = (BLK && x_div == 1) ? x + tile_off(m, k0 + x_c, (int)ldx) : x + xr * ldx + k0 + x_c;
+      const float* xp = (BLK && xblk) ? x + tile_off(m, k0 + x_c, (int)ldx) : x + xr * ldx + k0 + x_c;
       rx[p] = (m < m1 && x_valid > 0) ? load4_masked(xp, x_valid) : zero4;
     });
   };
@@ -1765,23 +1773,33 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf1
     p2[j] = (__bf16)r2;
   }
 }
-template <bool BLK>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
-__global__ void __launch_bounds__(512, 1)
+// HALF: the n rows split over two workgroups of 4 waves (one per SIMD), 128 rows each, two per CU:
+// the per-stage barrier then lines up only the 4 waves of one half, and the other workgroup's waves
+// on the same SIMDs (the other half, or another chunk) run out of phase, so one's split (VALU) can
+// run in the other's MFMA shadow.  The two halves of a chunk are launched 8 blocks apart (the same
+// XCD): the chunk's x rows come from HBM once per L2.  (512 threads: both halves in one workgroup.)
+template <bool BLK, bool HALF = false>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
+__global__ void __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1)
 wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
                    int clen, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
-  __shared__ double bsum[2][kWT];
-  const int chunk = blockIdx.x;
+  constexpr int NR = HALF ? kWT / 2 : kWT;           // a columns (output rows) of this workgroup
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][NR][kBfRow];
+  __shared__ double bsum[2][NR];
+  const int chunk = HALF ? (int)(blockIdx.x / 16) * 8 + (int)(blockIdx.x % 8) : (int)blockIdx.x;
   const int64_t m0 = (int64_t)chunk * clen;
+  if (m0 >= M) return;                               // (HALF: the grid's last 16-block group) uniform, before any barrier
   const int64_t m1 = m0 + clen < M ? m0 + clen : M;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wn = w & 1, wk = w >> 1;                 // n rows 128 wn .., k columns 64 wk ..
+  const int wn = HALF ? (int)(blockIdx.x / 8) % 2 : w & 1, wk = HALF ? w : w >> 1;   // n rows 128 wn .., k columns 64 wk ..
+  const int r0 = HALF ? 0 : 128 * wn;                // this wave's first row in As
+  const int n0 = HALF ? 128 * wn : 0;                // the workgroup's first output row
   const int h = lane >> 5, c = lane & 31;
-  // a loader: thread tid owns column tid % 256, samples 8 (tid / 256) .. +7 of each stage; sample j
+  // a loader: thread tid owns column tid % NR, samples 8 (tid / NR) .. +7 of each stage; sample j
   // of the octet at voffset avo + soffset j * lda4 (wave-uniform)
-  const int col = tid % kWT, oct = tid / kWT;
+  const int col = tid % NR, oct = tid / NR;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(col) + col % 8 + 64 * oct) : (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)col;
+  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(n0 + col) + col % 8 + 64 * oct)   // (n0 % 8 == 0)
+                          : (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)(n0 + col);
   const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
   uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
 #pragma unroll
@@ -1849,7 +1867,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
     for (int i = 0; i < 4; ++i) {
       bf16x8 fa[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[buf][p][128 * wn + 32 * i + c][8 * h]);
+      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[buf][p][r0 + 32 * i + c][8 * h]);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x16 t = acc[i][j];
@@ -1884,7 +1902,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   // bias column: every staged a value passed through store_a() exactly once (the rest are zeros)
   bsum[oct][col] = bacc;
   __syncthreads();
-  if (tid < kWT) out[(size_t)tid * KP + kWT] = (float)(bsum[0][tid] + bsum[1][tid]);
+  if (tid < NR) out[(size_t)(n0 + tid) * KP + kWT] = (float)(bsum[0][tid] + bsum[1][tid]);
 }
 
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
@@ -2008,13 +2026,15 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   if (h == 0) out[(size_t)(32 * w + c) * KP + K] = (float)bacc;
 }
 
+// x_blk: x tile-major (BLK and x_div == 1); under BLK a row-major x with x_div == 1 (the appearance
+// rows of one-sample "rays") takes the generic x loader, which reads row-major rows.
 template <int WN, int WK, bool BLK>
 static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
-                           int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
+                           bool x_blk, int64_t M, int chunks, int clen, float* ws, hipStream_t s) {
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
-  if (x_div == 1)
+  if (x_div == 1 && (!BLK || x_blk))
     hipLaunchKernelGGL((wgrad_bf_kernel<WN, WK, true, BLK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x,
                        ldx, K, x_div, M, ntk, tiles, chunks, clen, ws);
   else
@@ -2023,11 +2043,12 @@ static int launch_wgrad_bf(const float* a, int64_t lda, int N, const float* x, i
   return check_launch("wgrad_bf_kernel");
 }
 
-struct WgradSplit {                  // rows n >= n0 of a weight gradient belong to a second parameter
+struct WgradSplit {                  // rows n0 <= n < n_end of a weight gradient belong to a second parameter
   int n0 = 0;
   float* out_w = nullptr;            // its weight gradient, ld ldo, the first k columns
   int ldo = 0, k = 0;
   float* out_b = nullptr;            // its bias gradient (the bias column), nullable
+  int n_end = 1 << 30;               // rows from n_end on are dropped (padding rows of a whole-tile launch)
 };
 
 // out_w[n][k] (ld K) and out_b[n] (nullable) = (accumulate ? out : 0) + sum over chunks, in chunk
@@ -2069,6 +2090,7 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
     const int n = (int)(idx / KP), k = (int)(idx % KP);
     float* dst;
     if (split.out_w && n >= split.n0) {   // rows from n0 on belong to a second output (WgradSplit)
+      if (n >= split.n_end) continue;
       const int n2 = n - split.n0;
       dst = k < split.k ? split.out_w + (size_t)n2 * split.ldo + k : (k == K && split.out_b ? split.out_b + n2 : nullptr);
     } else {
@@ -2079,45 +2101,55 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
 }
 
 size_t wgrad_workspace_floats(int64_t M, int N, int K) {
-  const int clen = wgrad_chunk_len(N, K);   // >= the chunk count of every path of launch_wgrad
+  const int clen = wgrad_chunk_len(N, K, M);   // >= the chunk count of every path of launch_wgrad
   const int64_t chunks = (M + clen - 1) / clen;
   return (size_t)chunks * wgrad_stride(N, K);
 }
 
 template <int WN, int WK, bool BLK>
 static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div,
-                            int64_t M, int chunks, float* ws, hipStream_t s) {
+                            bool x_blk, int64_t M, int chunks, float* ws, hipStream_t s) {
   const int ntn = (N + 64 * WN - 1) / (64 * WN), ntk = (K + 64 * WK - 1) / (64 * WK);
   const int tiles = ntn * ntk;
   const int blocks = ((chunks + 7) / 8) * 8 * tiles;
   hipLaunchKernelGGL((wgrad_lds_kernel<WN, WK, BLK>), dim3((unsigned)blocks), dim3(256), 0, s, a, lda, N, x, ldx, K,
-                     x_div, M, ntk, tiles, chunks, ws);
+                     x_div, (int)(BLK && x_blk && x_div == 1), M, ntk, tiles, chunks, ws);
   return check_launch("wgrad_lds_kernel");
 }
 
-// tiled: a (and x when x_div == 1) are tile-major rows (layout.h) of row length lda / ldx, each
-// pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.
+// tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
+// each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
+// appearance projection's x (the embedding rows, one per ray) is row-major: x_tiled = false.
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
-                 const WgradSplit* split = nullptr, bool tiled = false) {
+                 const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true) {
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
   if (tiled && !(aligned && lda % 8 == 0 && (x_div != 1 || ldx % 8 == 0)))
     return set_error(NERF_ERR_BAD_ARG, "wgrad: tile-major operands must be aligned with row lengths % 8 == 0");
+  const bool x_blk = tiled && x_tiled && x_div == 1;   // x tile-major
   int rc;
   // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
-    const int clen = wgrad_chunk_len(N, K);
+    const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
-    if (wgrad_whole_tile(N, K) && x_div == 1) {
+    if (wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
+#ifndef NERF_WG_WHOLE   // two 4-wave workgroups per chunk (default; NERF_WG_WHOLE: one of 8 waves, A/B)
+      const unsigned hb = (unsigned)((chunks + 7) / 8) * 16;
+      if (tiled)
+        hipLaunchKernelGGL((wgrad_bf256_kernel<true, true>), dim3(hb), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
+      else
+        hipLaunchKernelGGL((wgrad_bf256_kernel<false, true>), dim3(hb), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
+#else
       if (tiled)
         hipLaunchKernelGGL(wgrad_bf256_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
       else
         hipLaunchKernelGGL(wgrad_bf256_kernel<false>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
+#endif
       rc = check_launch("wgrad_bf256_kernel");
-    } else if (N == kWT && K <= 64 && x_div == 1) {
+    } else if (N == kWT && K <= 64 && x_div == 1 && (!tiled || x_blk)) {
       if (tiled)
         hipLaunchKernelGGL(wgrad_bf_k64_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M,
                            clen, ws);
@@ -2126,18 +2158,18 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
                            clen, ws);
       rc = check_launch("wgrad_bf_k64_kernel");
     } else if (K <= 64 && N > 64) {
-      rc = tiled ? launch_wgrad_bf<4, 1, true>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s)
-                 : launch_wgrad_bf<4, 1, false>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+      rc = tiled ? launch_wgrad_bf<4, 1, true>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, clen, ws, s)
+                 : launch_wgrad_bf<4, 1, false>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, clen, ws, s);
     } else {
-      rc = tiled ? launch_wgrad_bf<2, 2, true>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s)
-                 : launch_wgrad_bf<2, 2, false>(a, lda, N, x, ldx, K, x_div, M, chunks, clen, ws, s);
+      rc = tiled ? launch_wgrad_bf<2, 2, true>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, clen, ws, s)
+                 : launch_wgrad_bf<2, 2, false>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, clen, ws, s);
     }
   } else if (aligned && K >= 1 && K <= 64 && N > 64) {
-    rc = tiled ? launch_wgrad_lds<4, 1, true>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s)
-               : launch_wgrad_lds<4, 1, false>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+    rc = tiled ? launch_wgrad_lds<4, 1, true>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, ws, s)
+               : launch_wgrad_lds<4, 1, false>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, ws, s);
   } else if (aligned && K >= 1) {
-    rc = tiled ? launch_wgrad_lds<2, 2, true>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s)
-               : launch_wgrad_lds<2, 2, false>(a, lda, N, x, ldx, K, x_div, M, chunks, ws, s);
+    rc = tiled ? launch_wgrad_lds<2, 2, true>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, ws, s)
+               : launch_wgrad_lds<2, 2, false>(a, lda, N, x, ldx, K, x_div, x_blk, M, chunks, ws, s);
   } else {
     const int tiles = ((N + 31) / 32) * ((KP + 63) / 64);
     hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((tiles + 3) / 4), (unsigned)chunks), dim3(256), 0, s, a, lda, N,
@@ -2183,6 +2215,30 @@ int launch_app_grad(const float* src, int64_t ld, int64_t rows, int group, const
   hipLaunchKernelGGL(app_grad_kernel, dim3((unsigned)rows), dim3(128), 0, s, src, ld, group, (int)tiled, packed, dapp);
   return check_launch("app_grad_kernel");
 }
+
+// ---------------------------------------------------------------- per-ray gradient sums
+// Inputs that are constant along a ray (PE_4(d) of dir_linear's last 27 columns, the appearance
+// row) make their weight gradient a GEMM over rays: sum_m g[m][n] x[ray(m)][k] = sum_r S[r][n] x[r][k]
+// with S[r] = sum over the ray's samples of g (distributivity; the sums in double).  Ray r's block:
+// S[r] = [sum d pre_dir (128) | sum d hd (128)] from the tile-major gradient rows, and E[r] = the
+// ray's PE_4(d) (its first sample's save row, kSaveEncD: 27 values + zeros) as a row-major row.
+__global__ void __launch_bounds__(256)
+ray_sums_kernel(const float* __restrict__ grad, const float* __restrict__ save, int N, float* __restrict__ S,
+                float* __restrict__ E) {
+  const int64_t r = blockIdx.x;
+  const int t = threadIdx.x;
+  const int col = t < kDirHidden ? kGradDir + t : kGradHd + (t - kDirHidden);
+  const int64_t m0 = r * N;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int j = 0; j < N; ++j) acc += (double)grad[tile_off(m0 + j, col, kGradRow)];
+  S[r * 256 + t] = (float)acc;
+  if (t < 32) E[r * 32 + t] = save[tile_off(m0, kSaveEncD + t, kSaveRow)];
+}
+
+// Floats of the ray-sum buffers (S, E) for any N >= kRaySumMinN: B = M / N <= M / kRaySumMinN rays.
+constexpr int kRaySumMinN = 32;
+static size_t ray_sum_floats(int64_t M) { return (size_t)(M / kRaySumMinN + 1) * (256 + 32) + 64; }
 
 // ------------------------------------------------------------------------------------ Adam
 // torch.optim.Adam (amsgrad=False, maximize=False, weight_decay=0) element for element:
@@ -2241,7 +2297,7 @@ enum { T_DIRS, T_Z, T_FEAT, T_ENCD, T_RGB, T_SIG, T_MAPS, T_DSIG, T_DRGB, T_SQE,
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// the largest wgrad partial buffer over the parameter list of param_grads
+// the largest wgrad partial buffer over the parameter list of param_grads, + the ray-sum buffers
 static size_t max_wgrad_floats(int64_t M) {
   const int Ks[] = {kPosEnc, kHidden, kHidden + kPosEnc, kHidden + kDirEnc, kAppDim, kDirHidden};
   size_t m = 0;
@@ -2249,7 +2305,7 @@ static size_t max_wgrad_floats(int64_t M) {
     const size_t f = wgrad_workspace_floats(M, kHidden, K);
     if (f > m) m = f;
   }
-  return m;
+  return m + ray_sum_floats(M);
 }
 
 // Which MLP arithmetic the last nerf_train_forward on a workspace ran under (the f32 forward writes no
@@ -2407,10 +2463,44 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
                            j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, ws, s, nullptr, true)))
       return rc;
   }
+  static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
+#ifndef NERF_NO_RAYSUM   // (A/B build: NERF_NO_RAYSUM keeps the M-row GEMMs for every N)
+  if (N >= kRaySumMinN) {
+#else
+  if (false) {
+#endif
+    // Rays of N >= 32 samples.  dir_linear's h7 columns and the density head (1 row over h7) run as
+    // one whole-tile 256 x 256 GEMM over a = the 256 gradient columns from d pre_dir on ([d pre_dir |
+    // d sigma | pad | d hd...]) and x = h7: rows 0..127 are dir_linear's gradient (+ its bias column),
+    // row 128 the density head's, rows 129.. are dropped (h7 is read once, on the fastest kernel).
+    // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over the
+    // B rays of the per-ray gradient sums (ray_sums_kernel), which replace two M-row GEMMs.
+    const int64_t B = M / N;
+    if (ws_floats < ray_sum_floats(M) || wgrad_workspace_floats(M, kWT, kWT) > ws_floats - ray_sum_floats(M))
+      return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+    const size_t wsf = (ws_floats - ray_sum_floats(M)) & ~(size_t)63;   // S, E 256-byte aligned
+    float* S = ws + wsf;                                   // B x 256
+    float* E = S + (size_t)B * 256;                        // B x 32
+    const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
+    if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kWT, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
+                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads, true)))
+      return rc;
+    hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, s, grad, save, N, S, E);
+    if ((rc = check_launch("ray_sums_kernel"))) return rc;
+    if ((rc = launch_wgrad(S, 256, kDirHidden, E, 32, kDirEnc, 1, B, g[P_DIR_W] + kHidden, kHidden + kDirEnc, nullptr,
+                           0, ws, s)))
+      return rc;
+    if (app_rows == 0) return NERF_OK;     // no appearance: the projection is unused (models.py:146)
+    if ((rc = launch_wgrad(S + kDirHidden, 256, kDirHidden, app, kAppDim, kAppDim, app_rows == 1 ? 0 : 1, B,
+                           g[P_APP_W], kAppDim, g[P_APP_B], 0, ws, s)))
+      return rc;
+    if (!dapp) return NERF_OK;
+    if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s, false);
+    return launch_app_grad(S + kDirHidden, 256, app_rows, 1, packed, dapp, s, false);
+  }
   // dir_linear (128 rows over [h7 | enc_d]) and the density head (1 row over h7) in one GEMM: the
   // gradient row holds [d pre_dir | d sigma], so rows 0..127 are dir_linear's gradient and row 128
   // (its first 256 columns and the bias column) the density head's: h7 is read once
-  static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
   if (wgrad_workspace_floats(M, kDirHidden + 1, kHidden + kDirEnc) > ws_floats)
     return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
   const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B]};
@@ -2423,7 +2513,7 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1; row-major)
   const int64_t xdiv = app_rows == 1 ? 0 : N;
   if ((rc = launch_wgrad(grad + tile_col(kGradHd), kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
-                         kAppDim, g[P_APP_B], 0, ws, s, nullptr, true)))
+                         kAppDim, g[P_APP_B], 0, ws, s, nullptr, true, /*x_tiled=*/false)))
     return rc;
   if (!dapp) return NERF_OK;
   if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s, false);

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 3 HEAD check on the GPU box: the whole GPU suite, the training bench, a same-box A/B of the
+# training step (row-major rows = HEAD~1, bound-scaled data gradient), the render bench, kernel trace.  Each step under its own limit; stops at the first crash/timeout.
+set -o pipefail
+mkdir -p gpurun_out
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -3 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread
+step bench_train 300 python bench_train.py --steps 20 --warmup 3 --no-cpu-baseline
+step ab_train 900 bash scripts/ab_train_libs.sh depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_rowmajor.so depth-aware-shader-effects-for-nerf_amd/build/ab/libnerfmi_tbound.so
+step bench 300 python bench.py --steps 5 --warmup 1
+ROOT=$(pwd)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_train" -o run -- python3 "$ROOT/bench_train.py" --steps 10 --warmup 2 --no-cpu-baseline > "$ROOT/gpurun_out/prof_train.log" 2>&1); echo "prof_train rc=$?"

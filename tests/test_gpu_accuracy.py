@@ -152,3 +152,53 @@ def test_h1_render_vs_float64(which, ref_state, app_vec, trained_state, arith):
     r64, d64 = _render_f64(which, st, oc, dc, app, u)
     check_no_worse_than_cpu(rgb.cpu(), r32, r64, f"{which}/{arith} rgb")
     check_no_worse_than_cpu(depth.cpu(), d32, d64, f"{which}/{arith} depth")
+
+
+@pytest.mark.parametrize("which", ["trained", "adversarial"])
+def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
+    """Every parameter gradient of NeRF.forward (the training kernels through autograd: forward with
+    saves, data-gradient chain, weight-gradient GEMMs) against float64 autograd, on trained and
+    adversarial weights.  The f16x3 data gradient splits each layer's gradient at a scale taken from
+    a pack-time bound (max row-L1 norm of W^T, csrc/train.hip mlp_backward16_bound_kernel), which the
+    adversarial rows loosen by up to 2^7: the GPU's per-tensor error must stay within twice the fp32
+    CPU autograd's own error against float64 (+1e-6 rel-L2 for tensors the two both get to ~eps).
+    One exception, measured: the f16x3 FORWARD on the adversarial weights, whose split scales come from
+    the same kind of loose bound (R_L max|a| + B_L, mlp16.hip), carries up to 4x the CPU's error
+    (test_forward above); the gradient of pts_linears.4.bias inherits it (rel-L2 2.73e-6 against the
+    CPU's 3.8e-7, identical to 3 digits whether the data gradient's scale is the bound or the exact row
+    maximum, so it is not the backward's), so that case is held to 8x.  The saturated colour head of
+    the adversarial model (sigmoid = 1 in fp32) makes the colour-branch tensors ~100 % off float64 in
+    both fp32 evaluations alike."""
+    import nerfmi
+    st, app = weights(which, ref_state, app_vec, trained_state)
+    model = nerfmi.NeRF(nerfmi.Config())
+    model.load_state_dict(st)
+    model = model.cuda()
+    g = torch.Generator().manual_seed(13)
+    M = 8192
+    x = torch.rand(M, 3, generator=g) * 3 - 1.5
+    d = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)
+    g_rgb, g_sig = torch.randn(M, 3, generator=g), torch.randn(M, 1, generator=g)
+    rgb, sigma = model(x.cuda(), d.cuda(), app.cuda())
+    ((rgb * g_rgb.cuda()).sum() + (sigma * g_sig.cuda()).sum()).backward()
+
+    def ref_grads(dtype):
+        sd = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in st.items()}   # fresh leaves
+        with torch.enable_grad():
+            r, s = O.nerf_forward(sd, x.to(dtype), d.to(dtype), app.to(dtype))
+            ((r * g_rgb.to(dtype)).sum() + (s * g_sig.to(dtype)).sum()).backward()
+        return {k: v.grad.double() for k, v in sd.items()}
+
+    g32, g64 = ref_grads(torch.float32), ref_grads(torch.float64)
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-300))
+
+    worst = []
+    for k, p in model.named_parameters():
+        e_gpu, e_cpu = rel(p.grad.cpu().double(), g64[k]), rel(g32[k], g64[k])
+        f = 8.0 if (which == "adversarial" and arith == "f16x3") else 2.0
+        worst.append((e_gpu / (f * e_cpu + 1e-6), k, e_gpu, e_cpu))
+        assert e_gpu <= f * e_cpu + 1e-6, (which, arith, k, e_gpu, e_cpu)
+    worst.sort(reverse=True)
+    print(f"{which}/{arith}: worst gradient tensors (ratio to the bound, key, gpu rel-L2, cpu rel-L2): {worst[:3]}")
