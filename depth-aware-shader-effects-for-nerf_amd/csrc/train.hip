@@ -769,10 +769,13 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
 // software-pipelined as in the forward's stream: a step's MFMAs run while the next step's 8
 // fragments are read, and the barrier that publishes chunk g+1 sits between chunk g's two steps:
 //   [read step 2c+1 (slot g) | MFMA step 2c] wait DMA(g+1), barrier, DMA(g+3) into the slot of
-//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]   -- i.e. bw_publish(g+1) issues
-//   DMA((g+1)+2) into chunk (g+1)-2's slot
-// (two chunks ahead in a 4-slot ring: every wave's reads of chunk g-2 fed MFMAs issued before the
-// publish(g) barrier, so DMA(g+2), issued right after that barrier, overwrites a free slot).  The
+//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]
+// where "publish(g+1)" = wait DMA(g+1), barrier, DMA(g+3): two chunks ahead of the chunk it
+// publishes, into slot (g+3) & 3 = the slot of chunk g-1 in the 4-slot ring.  Invariant: every
+// wave's reads of chunk g-1 fed MFMAs issued before the publish(g+1) barrier (they are the reads of
+// step 2c-1, done by the end of chunk g-1's steps), so the DMA issued right after that barrier
+// overwrites a free slot.  A deeper ring only needs the DMA distance and the slot count kept apart
+// by at least this one chunk.  The
 // stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then trunk
 // layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the kernel
 // reads M0 (as in mlp16.hip's stream).
@@ -1778,6 +1781,30 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf1
 // on the same SIMDs (the other half, or another chunk) run out of phase, so one's split (VALU) can
 // run in the other's MFMA shadow.  The two halves of a chunk are launched 8 blocks apart (the same
 // XCD): the chunk's x rows come from HBM once per L2.  (512 threads: both halves in one workgroup.)
+// Timing-only ablation builds (scripts/gpu_r03_*.sh; results are wrong): NERF_WG_NO_ALOAD / _NO_XLOAD
+// replace the operand loads by a constant, NERF_WG_NO_SPLIT the bf16 split by a bit cast.
+#ifdef NERF_WG_NO_ALOAD
+#define WG_LOAD_A(v) (0.5f)
+#else
+#define WG_LOAD_A(v) (v)
+#endif
+#ifdef NERF_WG_NO_XLOAD
+#define WG_LOAD_X(v) (0.25f)
+#else
+#define WG_LOAD_X(v) (v)
+#endif
+#ifdef NERF_WG_NO_SPLIT
+__device__ __forceinline__ void split3_cast(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  const f32x4 lo = {v[0], v[1], v[2], v[3]};
+  p0 = __builtin_bit_cast(bf16x8, lo);
+  const f32x4 hi = {v[4], v[5], v[6], v[7]};
+  p1 = __builtin_bit_cast(bf16x8, hi);
+  p2 = p0;
+}
+#define WG_SPLIT split3_cast
+#else
+#define WG_SPLIT split3_bf16
+#endif
 template <bool BLK, bool HALF = false>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
 __global__ void __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1)
 wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
@@ -1823,19 +1850,19 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0));
+      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0)));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0));
+        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0)));
   };
   auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
 #pragma unroll
     for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
     bf16x8 p0, p1, p2;
-    split3_bf16(ra[SET], p0, p1, p2);
+    WG_SPLIT(ra[SET], p0, p1, p2);
     *reinterpret_cast<bf16x8*>(&As[buf][0][col][8 * oct]) = p0;
     *reinterpret_cast<bf16x8*>(&As[buf][1][col][8 * oct]) = p1;
     *reinterpret_cast<bf16x8*>(&As[buf][2][col][8 * oct]) = p2;
@@ -1860,7 +1887,7 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
     const int buf = SET;
     bf16x8 fx[2][3];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) split3_bf16(rx[SET][t], fx[t][0], fx[t][1], fx[t][2]);
+    for (int t = 0; t < 2; ++t) WG_SPLIT(rx[SET][t], fx[t][0], fx[t][1], fx[t][2]);
     load(set_c, st + 2);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -2297,15 +2324,19 @@ enum { T_DIRS, T_Z, T_FEAT, T_ENCD, T_RGB, T_SIG, T_MAPS, T_DSIG, T_DRGB, T_SQE,
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// the largest wgrad partial buffer over the parameter list of param_grads, + the ray-sum buffers
-static size_t max_wgrad_floats(int64_t M) {
+// the largest wgrad partial buffer over the parameter list of param_grads (one stream's)
+static size_t wgrad_stream_floats(int64_t M) {
   const int Ks[] = {kPosEnc, kHidden, kHidden + kPosEnc, kHidden + kDirEnc, kAppDim, kDirHidden};
   size_t m = 0;
   for (int K : Ks) {
     const size_t f = wgrad_workspace_floats(M, kHidden, K);
     if (f > m) m = f;
   }
-  return m + ray_sum_floats(M);
+  return m;
+}
+// param_grads' workspace: two streams' partial buffers + the ray-sum buffers
+static size_t max_wgrad_floats(int64_t M) {
+  return 2 * ((wgrad_stream_floats(M) + 63) & ~(size_t)63) + ray_sum_floats(M) + 64;
 }
 
 // Which MLP arithmetic the last nerf_train_forward on a workspace ran under (the f32 forward writes no
@@ -2432,43 +2463,67 @@ int nerf_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, 
 
 // Every parameter gradient of NeRF (+ the appearance rows) from the saved activations and the
 // per-sample gradient rows; param_grads follows nerf_pack_weights' 24-pointer order.
-static int param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
-                       const float* packed, float* const* g, float* dapp, float* ws, size_t ws_floats,
-                       hipStream_t s) {
+//
+// Two streams.  The GEMMs are independent (each reads its slices of the save and gradient rows and
+// writes its own parameters), so they run on the caller's stream and on a second library stream,
+// each with its own partial buffer: one launch's tail, the small reductions and the memory-bound
+// ray sums overlap the other stream's GEMMs.  Every output is still written by one GEMM and one
+// fixed-order reduction (deterministic).  The second stream forks from the caller's after
+// everything queued there (the gradient rows) and the caller's stream waits for it at the end.
+struct PgStreams {
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static int pg_streams(PgStreams** out) {
+  static thread_local PgStreams per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return set_error(NERF_ERR_HIP, "param_grads: hipGetDevice");
+  PgStreams& p = per_dev[dev];
+  if (!p.s2) {
+    if (hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p.join, hipEventDisableTiming) != hipSuccess)
+      return set_error(NERF_ERR_HIP, "param_grads: stream/event creation failed");
+  }
+  *out = &p;
+  return NERF_OK;
+}
+
+// The jobs, on streams sa / sb with partial buffers wa / wb (wfl floats each) and the ray-sum
+// buffers at `rays` (N >= kRaySumMinN).
+static int param_grads_jobs(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
+                            const float* packed, float* const* g, float* dapp, float* wa, float* wb, size_t wfl,
+                            float* rays, hipStream_t sa, hipStream_t sb) {
   // Job: columns [k0, k0 + K) of parameter p's weight gradient (row length ldo) from x; the bias
   // gradient with the first column block only.  The skip layer's [h3 | enc_x] runs as a 256 x 256
   // block (the whole-tile kernel) plus the 63 PE columns, instead of one 256 x 319 GEMM on 128 x 128
   // tiles (416 -> ~300 us per step).
   // save and grad are tile-major rows (layout.h): a slice starting at feature c is the same layout at
-  // float offset tile_col(c)
-  struct Job { int a; int n; int x; int K; int p; int k0; int ldo; bool bias; };
+  // float offset tile_col(c).  Stream B: the K <= 64 GEMMs, layers 6-7 and the heads below.
+  struct Job { int a; int n; int x; int K; int p; int k0; int ldo; bool bias; bool b; };
   constexpr int kSkipK = kHidden + kPosEnc;
   const Job jobs[] = {
-      {0, kHidden, kSaveEncX, kPosEnc, 0, 0, kPosEnc, true},
-      {1 * kHidden, kHidden, save_h(0), kHidden, 2, 0, kHidden, true},
-      {2 * kHidden, kHidden, save_h(1), kHidden, 4, 0, kHidden, true},
-      {3 * kHidden, kHidden, save_h(2), kHidden, 6, 0, kHidden, true},
-      {4 * kHidden, kHidden, save_h(3), kHidden, 8, 0, kSkipK, true},                  // h3 ..
-      {4 * kHidden, kHidden, save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false},  // .. | enc_x
-      {5 * kHidden, kHidden, save_h(4), kHidden, 10, 0, kHidden, true},
-      {6 * kHidden, kHidden, save_h(5), kHidden, 12, 0, kHidden, true},
-      {7 * kHidden, kHidden, save_h(6), kHidden, 14, 0, kHidden, true},
-      {kGradRgb, 3, kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true},
+      {0, kHidden, kSaveEncX, kPosEnc, 0, 0, kPosEnc, true, true},
+      {1 * kHidden, kHidden, save_h(0), kHidden, 2, 0, kHidden, true, false},
+      {2 * kHidden, kHidden, save_h(1), kHidden, 4, 0, kHidden, true, false},
+      {3 * kHidden, kHidden, save_h(2), kHidden, 6, 0, kHidden, true, false},
+      {4 * kHidden, kHidden, save_h(3), kHidden, 8, 0, kSkipK, true, false},                  // h3 ..
+      {4 * kHidden, kHidden, save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false, true},  // .. | enc_x
+      {5 * kHidden, kHidden, save_h(4), kHidden, 10, 0, kHidden, true, false},
+      {6 * kHidden, kHidden, save_h(5), kHidden, 12, 0, kHidden, true, true},
+      {7 * kHidden, kHidden, save_h(6), kHidden, 14, 0, kHidden, true, true},
+      {kGradRgb, 3, kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true, false},
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
   for (const Job& j : jobs) {
-    if (wgrad_workspace_floats(M, j.n, j.K) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+    if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     if ((rc = launch_wgrad(grad + tile_col(j.a), kGradRow, j.n, save + tile_col(j.x), kSaveRow, j.K, 1, M, g[j.p] + j.k0,
-                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, ws, s, nullptr, true)))
+                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? wb : wa, j.b ? sb : sa, nullptr, true)))
       return rc;
   }
   static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
-#ifndef NERF_NO_RAYSUM   // (A/B build: NERF_NO_RAYSUM keeps the M-row GEMMs for every N)
-  if (N >= kRaySumMinN) {
-#else
-  if (false) {
-#endif
+  if (rays) {
     // Rays of N >= 32 samples.  dir_linear's h7 columns and the density head (1 row over h7) run as
     // one whole-tile 256 x 256 GEMM over a = the 256 gradient columns from d pre_dir on ([d pre_dir |
     // d sigma | pad | d hd...]) and x = h7: rows 0..127 are dir_linear's gradient (+ its bias column),
@@ -2476,36 +2531,34 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
     // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over the
     // B rays of the per-ray gradient sums (ray_sums_kernel), which replace two M-row GEMMs.
     const int64_t B = M / N;
-    if (ws_floats < ray_sum_floats(M) || wgrad_workspace_floats(M, kWT, kWT) > ws_floats - ray_sum_floats(M))
-      return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
-    const size_t wsf = (ws_floats - ray_sum_floats(M)) & ~(size_t)63;   // S, E 256-byte aligned
-    float* S = ws + wsf;                                   // B x 256
+    float* S = rays;                                       // B x 256
     float* E = S + (size_t)B * 256;                        // B x 32
+    if (wgrad_workspace_floats(M, kWT, kWT) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kWT, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
-                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads, true)))
+                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true)))
       return rc;
-    hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, s, grad, save, N, S, E);
+    hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, sb, grad, save, N, S, E);
     if ((rc = check_launch("ray_sums_kernel"))) return rc;
     if ((rc = launch_wgrad(S, 256, kDirHidden, E, 32, kDirEnc, 1, B, g[P_DIR_W] + kHidden, kHidden + kDirEnc, nullptr,
-                           0, ws, s)))
+                           0, wb, sb)))
       return rc;
     if (app_rows == 0) return NERF_OK;     // no appearance: the projection is unused (models.py:146)
     if ((rc = launch_wgrad(S + kDirHidden, 256, kDirHidden, app, kAppDim, kAppDim, app_rows == 1 ? 0 : 1, B,
-                           g[P_APP_W], kAppDim, g[P_APP_B], 0, ws, s)))
+                           g[P_APP_W], kAppDim, g[P_APP_B], 0, wb, sb)))
       return rc;
     if (!dapp) return NERF_OK;
-    if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s, false);
-    return launch_app_grad(S + kDirHidden, 256, app_rows, 1, packed, dapp, s, false);
+    if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, sb, false);
+    return launch_app_grad(S + kDirHidden, 256, app_rows, 1, packed, dapp, sb, false);
   }
   // dir_linear (128 rows over [h7 | enc_d]) and the density head (1 row over h7) in one GEMM: the
   // gradient row holds [d pre_dir | d sigma], so rows 0..127 are dir_linear's gradient and row 128
   // (its first 256 columns and the bias column) the density head's: h7 is read once
-  if (wgrad_workspace_floats(M, kDirHidden + 1, kHidden + kDirEnc) > ws_floats)
+  if (wgrad_workspace_floats(M, kDirHidden + 1, kHidden + kDirEnc) > wfl)
     return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
   const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B]};
   if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirHidden + 1, save + tile_col(save_h(7)), kSaveRow,
-                         kHidden + kDirEnc, 1, M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, ws, s, &heads, true)))
+                         kHidden + kDirEnc, 1, M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true)))
     return rc;
   if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
     return NERF_OK;
@@ -2513,11 +2566,42 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1; row-major)
   const int64_t xdiv = app_rows == 1 ? 0 : N;
   if ((rc = launch_wgrad(grad + tile_col(kGradHd), kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
-                         kAppDim, g[P_APP_B], 0, ws, s, nullptr, true, /*x_tiled=*/false)))
+                         kAppDim, g[P_APP_B], 0, wb, sb, nullptr, true, /*x_tiled=*/false)))
     return rc;
   if (!dapp) return NERF_OK;
-  if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, s, false);
-  return launch_app_grad(grad + tile_col(kGradHd), kGradRow, app_rows, N, packed, dapp, s, true);
+  if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, sb, false);
+  return launch_app_grad(grad + tile_col(kGradHd), kGradRow, app_rows, N, packed, dapp, sb, true);
+}
+
+static int param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
+                       const float* packed, float* const* g, float* dapp, float* ws, size_t ws_floats,
+                       hipStream_t s) {
+#ifndef NERF_NO_RAYSUM   // (A/B build: NERF_NO_RAYSUM keeps the M-row GEMMs for every N)
+  const bool ray_path = N >= kRaySumMinN;
+#else
+  const bool ray_path = false;
+#endif
+  const size_t rf = ray_path ? ray_sum_floats(M) : 0;
+  if (ws_floats < rf + 64) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+  const size_t avail = (ws_floats - rf) & ~(size_t)63;   // partial buffers; the ray sums after them, aligned
+  float* rays = ray_path ? ws + avail : nullptr;
+  const size_t w1 = (wgrad_stream_floats(M) + 63) & ~(size_t)63;
+#ifndef NERF_PG_ONE_STREAM   // (A/B build: every job on the caller's stream)
+  const bool two = avail >= 2 * w1;
+#else
+  const bool two = false;
+#endif
+  if (!two) return param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws, avail, rays, s, s);
+  PgStreams* ps;
+  int rc;
+  if ((rc = pg_streams(&ps))) return rc;
+  if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->s2, ps->fork, 0) != hipSuccess)
+    return set_error(NERF_ERR_HIP, "param_grads: stream fork failed");
+  rc = param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2);
+  // join even after a failed launch, so the caller's stream never runs ahead of queued work
+  if (hipEventRecord(ps->join, ps->s2) != hipSuccess || hipStreamWaitEvent(s, ps->join, 0) != hipSuccess)
+    return rc ? rc : set_error(NERF_ERR_HIP, "param_grads: stream join failed");
+  return rc;
 }
 
 int nerf_param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
