@@ -1932,6 +1932,153 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
   if (tid < NR) out[(size_t)(n0 + tid) * KP + kWT] = (float)(bsum[0][tid] + bsum[1][tid]);
 }
 
+// The 256 x 256 weight gradient with one wave per SIMD (mlp16's execution model instead of two
+// waves sharing each SIMD): a workgroup of 4 waves per 1,024-sample chunk, one per CU, each wave the
+// full 256 rows x 64 columns (8 x 2 MFMA tiles, 256 accumulator registers).  With the register file
+// to itself a wave keeps four stages of raw operands in flight (loads three stages ahead) and two
+// sets of split x fragments: stage st's MFMAs run while stage st+1's x and a are split (a into the
+// other LDS buffer) -- the VALU in the MFMA shadow of the same wave, not of a second wave that the
+// per-stage barrier lines up with it.  a: thread t loads column t (16 samples) and splits it once per
+// workgroup; x: each wave its own 64 columns in fragment order.  Same bf16x6 arithmetic, partial
+// layout and double bias column as wgrad_bf256_kernel.
+template <bool BLK>
+__global__ void __launch_bounds__(256, 1)
+wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
+                    int clen, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
+  const int chunk = blockIdx.x;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;   // wave wk: columns 64 wk ..
+  const int h = lane >> 5, c = lane & 31;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  // a loader: thread t owns column t, the stage's 16 samples: sample j at voffset avo + soffset j * as4
+  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(tid) + tid % 8) : 4u * (uint32_t)tid;
+  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
+  uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int xc = 64 * wk + 32 * t + c;
+    xvo[t] = BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)xc;
+  }
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[4][16], rx[4][2][8];      // four stages of raw operands: stage k in set k % 4
+  double bacc = 0.0;                 // bias column (column tid), in double
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;   // past the chunk: an empty resource, the loads read zeros
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0)));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0)));
+  };
+  bf16x8 fx[2][2][3];                // split x fragments of stages st (fx[st & 1]) and st+1
+  auto split_x = [&](auto set_c, auto fb_c) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value, FB = decltype(fb_c)::value;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) WG_SPLIT(rx[SET][t], fx[FB][t][0], fx[FB][t][1], fx[FB][t][2]);
+  };
+  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) bacc += (double)ra[SET][j];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ra[SET][8 * o + j];
+      bf16x8 p0, p1, p2;
+      WG_SPLIT(v, p0, p1, p2);
+      *reinterpret_cast<bf16x8*>(&As[buf][0][tid][8 * o]) = p0;
+      *reinterpret_cast<bf16x8*>(&As[buf][1][tid][8 * o]) = p1;
+      *reinterpret_cast<bf16x8*>(&As[buf][2][tid][8 * o]) = p2;
+    }
+  };
+  f32x16 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;   // a multiple of 4; extras read zeros
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+  load(C0{}, 0);
+  load(C1{}, 1);
+  load(C2{}, 2);
+  split_x(C0{}, C0{});
+  split_a(C0{}, 0);
+  __syncthreads();
+  // iteration st (set st % 4, buffers st % 2): stage st+3's loads; stage st's MFMAs with stage st+1's
+  // splits in their shadow; barrier
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value, FB = SET & 1;
+    using Nxt = std::integral_constant<int, (SET + 1) & 3>;
+    using Ld = std::integral_constant<int, (SET + 3) & 3>;
+    using FBn = std::integral_constant<int, FB ^ 1>;
+    load(Ld{}, st + 3);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * i + c][8 * h]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma_bf16(fa[0], fx[FB][j][2], t);
+        t = mfma_bf16(fa[1], fx[FB][j][1], t);
+        t = mfma_bf16(fa[2], fx[FB][j][0], t);
+        t = mfma_bf16(fa[0], fx[FB][j][1], t);
+        t = mfma_bf16(fa[1], fx[FB][j][0], t);
+        acc[i][j] = mfma_bf16(fa[0], fx[FB][j][0], t);
+      }
+    }
+    split_x(Nxt{}, FBn{});
+    split_a(Nxt{}, FB ^ 1);
+    // schedule: per row tile its 3 fragment reads, then its 12 MFMAs each followed by 2 VALU of the
+    // next stage's splits; the split's LDS writes last
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);     // VALU
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);         // DS writes
+    __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 4) {
+    iteration(C0{}, st);
+    iteration(C1{}, st + 1);
+    iteration(C2{}, st + 2);
+    iteration(std::integral_constant<int, 3>{}, st + 3);
+  }
+  constexpr int KP = kWT + 1;
+  float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = 64 * wk + 32 * j + c;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+    }
+  out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a exactly once
+}
+
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2163,7 +2310,12 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
     if (wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
-#ifndef NERF_WG_WHOLE   // two 4-wave workgroups per chunk (default; NERF_WG_WHOLE: one of 8 waves, A/B)
+#if !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
+      if (tiled)
+        hipLaunchKernelGGL(wgrad_bf256w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
+      else
+        hipLaunchKernelGGL(wgrad_bf256w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
+#elif defined(NERF_WG_HALF)   // A/B: two 4-wave workgroups per chunk (NERF_WG_WHOLE: one of 8 waves)
       const unsigned hb = (unsigned)((chunks + 7) / 8) * 16;
       if (tiled)
         hipLaunchKernelGGL((wgrad_bf256_kernel<true, true>), dim3(hb), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
