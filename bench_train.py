@@ -97,7 +97,8 @@ def pmc_traffic():
     try:
         k = json.load(open(PMC_SUMMARY))["kernels"]
         bw = next(v for n, v in k.items() if "mlp_backward16" in n)   # (the LDS-stream kernel since r02)
-        wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items() if "wgrad" in n)
+        wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items()
+                    if "wgrad" in n or "ray_sums" in n)   # the parameter-gradient phase (param_grads)
         return {"wgrad": wgrad / bw["dispatches"], "mlp_backward": bw["hbm_bytes_per_dispatch"]}
     except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
         return {}
