@@ -123,7 +123,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

@@ -45,7 +45,8 @@ const char* nerf_last_error(void);
 /* ABI version (bumped on any signature or layout change; 7: ReLU mask rows in the training forward
  * and backward, include/nerfmi_train.h; 8: nerf_frame_fog; 9: nerf_render_rays' ray0 (in-kernel
  * draws keyed by the global ray index), nerf_train_forward's weights/z outputs,
- * nerf_composite_backward_grad). */
+ * nerf_composite_backward_grad; 10: tile-major save / gradient rows, NERF_TILE_ROWS, and the
+ * two-stream nerf_param_grads with its larger workspace). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays

@@ -144,21 +144,47 @@ def check_mask_words(sv, mk):
                         assert np.array_equal(got, act[:, 32 * T + 8 * q + 4 * hh + e]), (w0, hh, T, q, e)
 
 
-def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
-    """GPU forward-with-saves + data-gradient chain on random points, and the float64 autograd of
-    the oracle's NeRF.forward on the same points."""
-    L = _lib()
-    lib, dev = L.load(), L.device()
+def _draw(R, N, seed):
+    """Random rays (o, d, sorted z in [2, 6]) and upstream gradients of their R*N samples."""
     g = torch.Generator().manual_seed(seed)
     o = torch.randn(R, 3, generator=g) * 0.3
     d = F.normalize(torch.randn(R, 3, generator=g), dim=-1)
     z = torch.sort(2 + 4 * torch.rand(R, N, generator=g), dim=-1).values
+    return o, d, z, torch.randn(R * N, 3, generator=g), torch.randn(R * N, generator=g)
+
+
+def _safe_draw(state, app, R, N, seed, rel=1e-5):
+    """_draw, keeping only rays none of whose float64 ReLU pre-activations lies within rel x (that
+    layer's rms) of the kink: there an fp32 evaluation may land on either side (the CPU's and the
+    GPU's roundings differ by host), which moves that sample's whole gradient chain and makes a
+    tensor's error a lottery instead of a measurement."""
+    o, d, z, gr, gs = _draw(4 * R, N, seed)
+    pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
+    dexp = d[:, None, :].expand(4 * R, N, 3).reshape(-1, 3)
+    a = None if app is None else (app.double() if app.dim() == 1 else None)
+    pres = []
+    with torch.no_grad():
+        O.nerf_forward({k: v.double() for k, v in state.items()}, pts.double(), dexp.double(), a, keep=pres)
+    ok = torch.ones(4 * R, dtype=torch.bool)
+    for p_ in pres:
+        ok &= ((p_.abs() / p_.pow(2).mean().sqrt()) > rel).reshape(4 * R, -1).all(dim=1)
+    keep = torch.nonzero(ok)[:, 0][:R]
+    assert keep.numel() == R, f"only {keep.numel()} of {4 * R} rays clear the ReLU kinks"
+    samp = (keep[:, None] * N + torch.arange(N)).reshape(-1)
+    return o[keep], d[keep], z[keep], gr[samp], gs[samp]
+
+
+def _mlp_forward_backward(state, app, R=96, N=11, seed=3, draw=None):
+    """GPU forward-with-saves + data-gradient chain on random points, and the float64 autograd of
+    the oracle's NeRF.forward on the same points (draw: the rays and upstream gradients, else _draw)."""
+    L = _lib()
+    lib, dev = L.load(), L.device()
+    o, d, z, g_rgb, g_sigma = _draw(R, N, seed) if draw is None else draw
     M = R * N
-    g_rgb = torch.randn(M, 3, generator=g)
-    g_sigma = torch.randn(M, generator=g)
     packed, packedT, _ = packed_of(state, dev)
     og, dg, zg = o.to(dev), d.to(dev), z.to(dev).contiguous()
-    a, rows = (None, 0) if app is None else (app.reshape(1, 32).to(dev).contiguous(), 1)
+    per_ray = app is not None and app.dim() == 2 and app.shape[0] == R   # one appearance row per ray
+    a, rows = (None, 0) if app is None else (app.reshape(-1, 32).to(dev).contiguous(), R if per_ray else 1)
     feat, encd = torch.empty(R, 256, device=dev), torch.empty(R, 32, device=dev)
     rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
     save = torch.empty(L.tile_rows(M), L.SAVE_ROW, device=dev)
@@ -191,7 +217,8 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3):
     dexp = d[:, None, :].expand(R, N, 3).reshape(-1, 3)
     st64 = {k: v.double().requires_grad_(True) for k, v in state.items()}
     pres = []
-    rgb_o, sigma_o = O.nerf_forward(st64, pts.double(), dexp.double(), None if app is None else app.double(),
+    app_o = None if app is None else (app[:, None, :].expand(R, N, 32).reshape(-1, 32) if per_ray else app)
+    rgb_o, sigma_o = O.nerf_forward(st64, pts.double(), dexp.double(), None if app is None else app_o.double(),
                                     keep=pres)
     for t in pres:
         t.retain_grad()
@@ -255,6 +282,71 @@ def test_param_grads_match_autograd(ref_state, app_vec, with_app):
             continue
         exp = r["st64"][k].grad.numpy()
         assert rel_l2(gt.cpu().numpy(), exp) < 2e-4, (k, rel_l2(gt.cpu().numpy(), exp))
+
+
+def _oracle_grads_f32(state, app, R, N, draw):
+    """The oracle's fp32 autograd on _mlp_forward_backward's points and upstream gradients."""
+    o, d, z, g_rgb, g_sigma = draw
+    pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
+    dexp = d[:, None, :].expand(R, N, 3).reshape(-1, 3)
+    per_ray = app is not None and app.dim() == 2 and app.shape[0] == R
+    app_o = None if app is None else (app[:, None, :].expand(R, N, 32).reshape(-1, 32) if per_ray else app)
+    sd = {k: v.detach().clone().float().requires_grad_(True) for k, v in state.items()}
+    with torch.enable_grad():
+        rgb_o, sigma_o = O.nerf_forward(sd, pts, dexp, app_o)
+        ((rgb_o * g_rgb).sum() + (sigma_o[:, 0] * g_sigma).sum()).backward()
+    return {k: v.grad.numpy() for k, v in sd.items() if v.grad is not None}
+
+
+@pytest.mark.parametrize("app_kind", ["broadcast", "per_ray", "none"])
+def test_param_grads_ray_path(ref_state, app_vec, app_kind):
+    """nerf_param_grads with N >= 32 samples per ray: the per-ray gradient sums (dir_linear's PE_4(d)
+    columns, the appearance projection and the appearance rows as GEMMs over rays), dir/sigma on the
+    whole-tile GEMM, the two-stream schedule.  N = 40 so tile-major blocks straddle rays; against the
+    oracle's float64 autograd, and two calls bit-identical (fixed-order reductions on both streams)."""
+    L = _lib()
+    lib, dev = L.load(), L.device()
+    R, N = 48, 40
+    app = {"broadcast": app_vec, "per_ray": torch.randn(R, 32, generator=torch.Generator().manual_seed(5)),
+           "none": None}[app_kind]
+    draw = _safe_draw(ref_state, app, R, N, seed=3)
+    r = _mlp_forward_backward(ref_state, app, R=R, N=N, draw=draw)
+    save, grad = r["save_tiled"].to(dev), r["grad_tiled"].to(dev)
+    packed, _, ts = packed_of(ref_state, dev)
+    M = R * N
+    rows = 0 if app is None else (R if app_kind == "per_ray" else 1)
+    a = None if app is None else app.reshape(-1, 32).to(dev).contiguous()
+    ws = torch.empty(lib.nerf_param_grads_workspace_bytes(M), dtype=torch.uint8, device=dev)
+    runs = []
+    for _ in range(2):
+        grads = [torch.full_like(t, float("nan")) for t in ts]
+        arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in grads])
+        dapp = torch.full((max(rows, 1), 32), float("nan"), device=dev)
+        L.check(lib.nerf_param_grads(L.ptr(save), L.ptr(grad), M, N, L.ptr(a), rows, L.ptr(packed), arr, L.ptr(dapp),
+                                     L.ptr(ws), ws.numel(), L.stream()), "param_grads")
+        torch.cuda.synchronize()
+        runs.append(([g.cpu() for g in grads], dapp.cpu()))
+    for k, g1, g2 in zip(O.STATE_KEYS, runs[0][0], runs[1][0]):
+        if app is None and k.startswith("appearance_projection"):
+            continue                                               # not on the path: left untouched
+        assert torch.equal(g1, g2), k
+    assert rows == 0 or torch.equal(runs[0][1], runs[1][1])
+    # (rays near a ReLU kink are not drawn, _safe_draw; each tensor is held to 2e-4 or twice the CPU
+    # fp32 autograd's error, whichever is larger)
+    g32 = _oracle_grads_f32(ref_state, app, R, N, draw)
+    for k, gt in zip(O.STATE_KEYS, runs[0][0]):
+        if app is None and k.startswith("appearance_projection"):
+            continue
+        exp = r["st64"][k].grad.numpy()
+        e_gpu, e_cpu = rel_l2(gt.numpy(), exp), rel_l2(g32[k], exp)
+        assert e_gpu < max(2e-4, 2 * e_cpu), (k, e_gpu, e_cpu)
+    if rows:
+        # d app_row(r) = W_app^T sum over the ray's samples of d hd (broadcast: over all samples)
+        W = r["st64"]["appearance_projection.weight"].detach()
+        dhd = r["grad"][:, 2184:2312].double()                        # layout.h kGradHd
+        s_r = dhd.reshape(R, N, 128).sum(1) if rows == R else dhd.sum(0, keepdim=True)
+        exp_app = (s_r @ W).numpy()
+        assert rel_l2(runs[0][1].numpy(), exp_app) < 1e-5, rel_l2(runs[0][1].numpy(), exp_app)
 
 
 def test_wgrad_generic_shapes():
