@@ -1292,7 +1292,8 @@ constexpr int kWChunk = 2048;   // samples per chunk
 // and the appearance projection) hold one block per CU and have one tile: 1024-sample chunks give
 // 256 blocks instead of 128.  The 128x128-tile launches hold two blocks per CU; those with fewer
 // than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
-static inline bool wgrad_whole_tile(int N, int K) { return N == 256 && K == 256; }
+// (N = 160: dir_linear's 128 rows + the density head's, the tile-major training path only)
+static inline bool wgrad_whole_tile(int N, int K) { return (N == 256 || N == 160) && K == 256; }
 static inline int wgrad_chunk_len_big(int N, int K) {
   if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
   if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
@@ -1941,7 +1942,9 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
 // per-stage barrier lines up with it.  a: thread t loads column t (16 samples) and splits it once per
 // workgroup; x: each wave its own 64 columns in fragment order.  Same bf16x6 arithmetic, partial
 // layout and double bias column as wgrad_bf256_kernel.
-template <bool BLK>
+// NRT: output row tiles (8 = 256 rows; 5 = 160 rows, dir_linear + the density head: the a loader still
+// stages 256 columns, the MFMAs and the partial cover the first 32 NRT rows).
+template <bool BLK, int NRT = 8>
 __global__ void __launch_bounds__(256, 1)
 wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
                     int clen, float* __restrict__ partial) {
@@ -2006,9 +2009,9 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
       *reinterpret_cast<bf16x8*>(&As[buf][2][tid][8 * o]) = p2;
     }
   };
-  f32x16 acc[8][2];
+  f32x16 acc[NRT][2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
   const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;   // a multiple of 4; extras read zeros
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
@@ -2029,7 +2032,7 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     load(Ld{}, st + 3);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NRT; ++i) {
       bf16x8 fa[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * i + c][8 * h]);
@@ -2049,12 +2052,12 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     // schedule: per row tile its 3 fragment reads, then its 12 MFMAs each followed by 2 VALU of the
     // next stage's splits; the split's LDS writes last
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NRT; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads
 #pragma unroll
       for (int k = 0; k < 12; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);     // VALU
+        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 4, 0);     // VALU
       }
     }
     __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);         // DS writes
@@ -2067,16 +2070,16 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     iteration(std::integral_constant<int, 3>{}, st + 3);
   }
   constexpr int KP = kWT + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
+  float* out = partial + (size_t)chunk * wgrad_stride(32 * NRT, kWT);
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NRT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int kk = 64 * wk + 32 * j + c;
 #pragma unroll
       for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
     }
-  out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a exactly once
+  if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a once
 }
 
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
@@ -2309,7 +2312,11 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
-    if (wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
+    if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
+      hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
+                         ws);
+      rc = check_launch("wgrad_bf256w_kernel<5>");
+    } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
 #if !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
       if (tiled)
         hipLaunchKernelGGL(wgrad_bf256w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
@@ -2677,17 +2684,18 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
   if (rays) {
     // Rays of N >= 32 samples.  dir_linear's h7 columns and the density head (1 row over h7) run as
-    // one whole-tile 256 x 256 GEMM over a = the 256 gradient columns from d pre_dir on ([d pre_dir |
-    // d sigma | pad | d hd...]) and x = h7: rows 0..127 are dir_linear's gradient (+ its bias column),
-    // row 128 the density head's, rows 129.. are dropped (h7 is read once, on the fastest kernel).
+    // one 160 x 256 GEMM on the whole-tile kernel (5 row tiles) over a = the gradient columns from
+    // d pre_dir on ([d pre_dir | d sigma | pad | d hd...]) and x = h7: rows 0..127 are dir_linear's
+    // gradient (+ its bias column), row 128 the density head's, rows 129.. are dropped (h7 is read once).
     // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over the
     // B rays of the per-ray gradient sums (ray_sums_kernel), which replace two M-row GEMMs.
     const int64_t B = M / N;
     float* S = rays;                                       // B x 256
     float* E = S + (size_t)B * 256;                        // B x 32
-    if (wgrad_workspace_floats(M, kWT, kWT) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+    constexpr int kDirRows = 160;
+    if (wgrad_workspace_floats(M, kDirRows, kWT) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
-    if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kWT, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
+    if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
                            M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true)))
       return rc;
     hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, sb, grad, save, N, S, E);

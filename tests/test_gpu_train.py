@@ -357,7 +357,8 @@ def test_wgrad_generic_shapes():
     g = torch.Generator().manual_seed(9)
     for (M, N, K, xdiv) in [(1, 1, 1, 1), (4099, 33, 70, 1), (5000, 3, 128, 1), (3000, 128, 32, 10), (777, 5, 9, 0),
                             # the whole-tile and K <= 64 kernels on a partial chunk / ragged chunks
-                            (700, 256, 256, 1), (33, 256, 256, 1), (5003, 256, 40, 1), (17, 256, 64, 1),
+                            (700, 256, 256, 1), (33, 256, 256, 1), (3000, 160, 256, 1), (5003, 256, 40, 1),
+                            (17, 256, 64, 1),
                             # the production step's shapes: 4096 rays x 64 samples = 262,144 rows
                             (262144, 256, 256, 1), (262144, 256, 63, 1), (262144, 3, 128, 1),
                             (262144, 128, 32, 64), (262147, 1, 256, 1),
