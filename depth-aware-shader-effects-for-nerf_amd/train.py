@@ -113,6 +113,8 @@ class Trainer:
         self.steps = 0
         self._ws = None
         self._tvals = {}
+        self._side = None          # side stream for the transposed packing (forward_backward)
+        self._side_on = os.environ.get("NERFMI_PACKT_SIDE", "1") != "0"   # (0: same-box A/B)
 
     def view(self, buf, i):
         return buf[self.offsets[i]: self.offsets[i + 1]].view(self.shapes[i])
@@ -140,8 +142,18 @@ class Trainer:
         if seed is None:
             seed = step_seed(self.steps + 1, self.rank)
         _lib.check(lib.nerf_pack_weights(self.param_ptrs, P(self.packed), s), "nerf_pack_weights")
-        _lib.check(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), s),
+        # The transposed weights are read only by the backward: they are packed on a side stream while
+        # the forward runs (forked after everything queued so far, so after the previous step's
+        # backward read them; joined before this step's backward).
+        main = torch.cuda.current_stream(self.dev)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev) if self._side_on else main
+            self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
+        self._fork.record(main)
+        self._side.wait_event(self._fork)
+        _lib.check(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), self._side.cuda_stream),
                    "nerf_pack_weights_transposed")
+        self._join.record(self._side)
         if N not in self._tvals:
             self._tvals[N] = linspace_table(N, self.dev)
         ws = self._workspace(B, N)
@@ -160,6 +172,7 @@ class Trainer:
         if self.app_grad is not None:
             self.app_grad.zero_()
         dapp = self.dapp if rows else None
+        main.wait_event(self._join)
         _lib.check(lib.nerf_train_backward(P(self.packed), P(self.packedT), P(rgb_map), P(tgt), B, N, P(app), rows,
                                            self.grad_ptrs, P(dapp), P(self.loss_buf), P(ws), ws.numel(), s),
                    "nerf_train_backward")
