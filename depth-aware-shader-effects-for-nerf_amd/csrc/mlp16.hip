@@ -150,8 +150,12 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     }
   }
   if constexpr (SV) {
+#ifndef NERF_FWD_NO_SAVES   // (timing-only A/B builds: without the activation stores / the mask bits)
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
+#endif
+#ifndef NERF_FWD_NO_MASKS
     mask_or(sv, T, bits);
+#endif
   }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
