@@ -541,6 +541,35 @@ def test_training_reduces_loss_on_teacher_scene():
     assert np.mean(losses[-5:]) < 0.7 * np.mean(losses[:5]), losses
 
 
+def test_training_is_deterministic():
+    """Two trainers from the same seed, 25 production-size steps (4,096 rays x 64 samples) each: the
+    parameters, Adam moments and losses are bit-identical.  Every kernel of the step (the LDS-DMA
+    weight streams with stores in flight, the two-stream parameter gradients, the side-stream
+    packing) must order its memory exactly; a race shows up here as a difference, not as a tolerance
+    miss."""
+    import nerfmi
+    from nerfmi.dataset import SyntheticNeRFDataset
+    from nerfmi.train import Trainer
+    cfg = nerfmi.Config()
+    runs = []
+    for _ in range(2):
+        np.random.seed(0)
+        torch.manual_seed(0)                        # (the dataset draws its appearance table from torch's RNG)
+        ds = SyntheticNeRFDataset(cfg, n_images=3, H=96, W=96)
+        torch.manual_seed(0)
+        tr = Trainer(cfg, appearance_embeddings=ds.appearance_embeddings)
+        losses = []
+        for i in range(25):
+            b = ds.get_rays(batch_size=4096)        # np.random, seeded above: the same batches both runs
+            losses.append(float(tr.step(b["rays_o"], b["rays_d"], b["rgb"], b["appearance_idx"], seed=i + 1)))
+        torch.cuda.synchronize()
+        runs.append((tr.flat.detach().cpu().clone(), tr.exp_avg.detach().cpu().clone(),
+                     tr.exp_avg_sq.detach().cpu().clone(), losses))
+    assert runs[0][3] == runs[1][3]
+    for a_, b_ in zip(runs[0][:3], runs[1][:3]):
+        assert torch.equal(a_, b_)
+
+
 def test_production_batch_matches_oracle(ref_state, app_vec):
     """The production step (config 5, train.py:77-92): 4096 rays x 64 samples = 262,144 MLP rows,
     the regime where the weight gradients run as 128 XCD-grouped chunks x 4 tiles with the
