@@ -29,8 +29,8 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-DEFAULT_KERNELS = r"mlp16_kernel|mlp_backward16"
-DEFAULT_STREAMS = r"mlp16_kernel|mlp_backward16_lds|mlp_backward16_bound"
+DEFAULT_KERNELS = r"mlp16_kernel|mlp_backward16|wgrad_dma256"
+DEFAULT_STREAMS = r"mlp16_kernel|mlp_backward16_lds|mlp_backward16_bound|wgrad_dma256"
 IMPLICIT_M0 = re.compile(r"^(s_movrel|v_movrel|s_set_gpr_idx|ds_\w*addtid|ds_gws_|ds_append|ds_consume|"
                          r"ds_ordered_count|s_sendmsg|v_interp|s_ttracedata)")
 LDS_DMA = re.compile(r"^(global_load_lds_|buffer_load_\w+.*\blds\b|buffer_load_lds_)")
