@@ -52,7 +52,6 @@ def trained_state():
     try:
         cfg = nerfmi.Config()
         np.random.seed(0)
-        torch.manual_seed(0)   # the dataset's appearance table: independent of the tests run before
         ds = SyntheticNeRFDataset(cfg, n_images=8, H=96, W=96)
         torch.manual_seed(0)
         tr = Trainer(cfg, appearance_embeddings=ds.appearance_embeddings)
@@ -177,21 +176,8 @@ def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
     model = model.cuda()
     g = torch.Generator().manual_seed(13)
     M = 8192
-    x = torch.rand(2 * M, 3, generator=g) * 3 - 1.5
-    d = torch.nn.functional.normalize(torch.randn(2 * M, 3, generator=g), dim=-1)
-    # keep the points none of whose float64 ReLU pre-activations lies within 1e-5 x (that layer's rms)
-    # of the kink: there the CPU's and the GPU's fp32 roundings may land on opposite sides, which moves
-    # the point's whole gradient chain (one such point put pts_linears.0.weight 6.5e-4 off on one set of
-    # trained weights) and turns the comparison into a lottery instead of a measurement
-    pres = []
-    with torch.no_grad():
-        O.nerf_forward({k: v.double() for k, v in st.items()}, x.double(), d.double(), app.double(), keep=pres)
-    ok = torch.ones(2 * M, dtype=torch.bool)
-    for p_ in pres:
-        ok &= ((p_.abs() / p_.pow(2).mean().sqrt()) > 1e-5).reshape(2 * M, -1).all(dim=1)
-    sel = torch.nonzero(ok)[:, 0][:M]
-    assert sel.numel() == M, f"only {sel.numel()} of {2 * M} points clear the ReLU kinks"
-    x, d = x[sel], d[sel]
+    x = torch.rand(M, 3, generator=g) * 3 - 1.5
+    d = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1)
     g_rgb, g_sig = torch.randn(M, 3, generator=g), torch.randn(M, 1, generator=g)
     rgb, sigma = model(x.cuda(), d.cuda(), app.cuda())
     ((rgb * g_rgb.cuda()).sum() + (sigma * g_sig.cuda()).sum()).backward()
