@@ -2143,8 +2143,9 @@ wgrad_dma256_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   // DMA: this wave's pieces j = 4 wk .. 4 wk + 3; lane l copies 16 bytes of group j + 16 (l / 32)
   const uint32_t voff = (uint32_t)(4 * wk + 16 * h) * 1024u + (uint32_t)c * 16u;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-  auto issue = [&](int st) __attribute__((always_inline)) {
-    const int64_t ms = m0 + 16 * (int64_t)st;
+  // stage st's image <- stage src's samples (src = st except past the chunk's end, see publish)
+  auto issue = [&](int st, int src) __attribute__((always_inline)) {
+    const int64_t ms = m0 + 16 * (int64_t)src;
     const char* sa = reinterpret_cast<const char*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8);
     const char* sx = reinterpret_cast<const char*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8);
     const uint32_t dst = ring_lds + (uint32_t)(st % kDmaStages) * kDmaStage + (uint32_t)(4 * wk) * kDmaSlot;
@@ -2176,20 +2177,24 @@ wgrad_dma256_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     const float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
     bacc[i] += (double)(s * keep);
   };
-  // publish(st): this wave's pieces of stage st landed (younger: those of st+1 when issued), barrier,
+  // publish(st): this wave's pieces of stage st landed (younger: exactly those of st+1), barrier,
   // then stage st+2's pieces into the image of stage st-2.  Stage st+1 is published while stage st
   // is computed, so the next stage's first a tile and x fragments are read in this stage's shadow.
+  // Branch-free: a stage past the chunk re-reads the chunk's last stage into its (free) image, so the
+  // wait is always vmcnt(8) and every path through the kernel issues and publishes the same pieces
+  // (scripts/check_isa.py proves the counts on the ISA's control-flow graph; a conditional issue
+  // would give it paths the hardware never takes).  The pieces still in flight at the end are
+  // drained before the partial is written.
   auto publish = [&](int st) __attribute__((always_inline)) {
-    if (st + 1 < nst) wait_vmcnt<8>();
-    else wait_vmcnt<0>();
+    wait_vmcnt<8>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (st + 2 < nst) issue(st + 2);
+    issue(st + 2, st + 2 < nst ? st + 2 : nst - 1);
   };
-  if (0 < nst) issue(0);
-  if (1 < nst) issue(1);
+  issue(0, 0);
+  issue(1, 1 < nst ? 1 : 0);
   publish(0);
   float vb[8], vx[2][8];              // raw: the next tile's a fragment, the next stage's x
   bf16x8 fa[3], fx[2][3], fxn[2][3];  // split: this tile's a, this stage's x, the next stage's x
@@ -2249,6 +2254,7 @@ wgrad_dma256_kernel(const float* __restrict__ a, int64_t lda, const float* __res
 #pragma unroll
       for (int q = 0; q < 3; ++q) fx[t][q] = fxn[t][q];
   }
+  wait_vmcnt<0>();                   // the past-the-end pieces land before the workgroup's LDS is released
   constexpr int KP = kWT + 1;
   float* out = partial + (size_t)chunk * wgrad_stride(32 * NRT, kWT);
 #pragma unroll

@@ -16,8 +16,13 @@ translation unit) and checks, in every kernel whose name matches --kernels:
   * the stream kernels (--streams) hold at least one DMA piece (the pattern is still what the
     stream emits).
 
-Exit status 0 = clean; 1 = a violation (listed).  `make check-isa` runs it; tests/test_check_isa.py
-runs it on the built library and on a disassembly with an M0 reader inserted.
+and, in the stream kernels (STREAM_PIECES), that every counted `s_waitcnt vmcnt(N)` publishing an
+LDS-DMA ring slot leaves in flight only pieces younger than the published chunk, on every path of the
+kernel's control-flow graph (check_vmcnt, below).
+
+Exit status 0 = clean; 1 = a violation (listed).  `make check-isa` and __graft_entry__.build() run it;
+tests/test_check_isa.py runs it on the built library, on disassemblies with an M0 reader inserted or a
+publish over-counted, and on committed disassemblies of known-good and known-bad builds.
 """
 import argparse
 import os
@@ -137,9 +142,186 @@ def check_function(insns):
     return bad, pieces
 
 
+# ---- counted vmcnt waits of the LDS-DMA streams --------------------------------------------------
+# A stream kernel publishes ring slots with `s_waitcnt vmcnt(N)` + `s_barrier`: hipcc does not count
+# the asm DMA pieces, so N is written by hand as "the pieces and stores issued after the awaited
+# ones".  vmcnt retires loads, stores, atomics and LDS-DMA together in issue order (flat_* excepted),
+# so the ops that may still be outstanding after vmcnt(N) are the N youngest issued.  The stream
+# protocol: the b-th s_barrier after the kernel's first piece publishes the b-th group of P pieces
+# (P = this wave's pieces per chunk / stage), so before it every piece of groups 0..b must be done:
+#     (pieces possibly outstanding) <= (pieces issued) - P (b + 1).
+# check_vmcnt walks the kernel's control-flow graph with the set of possible (issued - P b,
+# outstanding-op sequence) states per block and checks that inequality at every barrier, on every
+# path; it also rejects a flat_* op while a DMA piece may be outstanding, and a DMA piece still
+# possibly outstanding at s_endpgm.  A count one too large (a store counted as younger than the
+# awaited pieces that the scheduler placed before them) fails it; counting fewer is always safe.
+# The outstanding sequence is kept 63 deep: the counter holds at most 63 ops and issue stalls on a
+# full counter, so an op with 63 younger ones has retired.  Instructions whose vmcnt effect is not
+# certain are not counted (counting an op that the hardware does not would be the unsafe direction).
+STREAM_PIECES = (  # (kernel regex, this wave's pieces per published chunk / stage)
+    (r"mlp16_kernel", 4),
+    (r"mlp_backward16_lds_kernel", 4),
+    (r"mlp_backward16_bound_kernel", 4),
+    (r"wgrad_dma256_kernel", 8),
+)
+VM_OP = re.compile(r"^(global_|buffer_(load|store|atomic)|scratch_)")
+FLAT_OP = re.compile(r"^flat_")
+BRANCH = re.compile(r"^s_(c?branch\w*)")
+MAX_STATES = 4096          # per block: a blow-up means the states diverge (a loop that gains pieces)
+
+
+def _instructions(text):
+    """{kernel: [(address, instruction, branch target or None)]} from llvm-objdump -d -C output."""
+    funcs, cur, base = {}, None, 0
+    for line in text.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.*)>:$", line)
+        if m:
+            cur, base = m.group(2), int(m.group(1), 16)
+            funcs[cur] = []
+            continue
+        if cur is None:
+            continue
+        s = line.strip()
+        if not s or s.startswith(";") or s.endswith(":") or "//" not in s:
+            continue
+        ins, comment = s.split("//", 1)
+        ins = ins.strip()
+        am = re.match(r"\s*([0-9A-Fa-f]+):", comment)
+        if not ins or not am:
+            continue
+        tgt = None
+        tm = re.search(r"<.*\+(0x[0-9a-f]+)>\s*$", comment)
+        if BRANCH.match(ins) and tm:
+            tgt = base + int(tm.group(1), 16)
+        elif BRANCH.match(ins) and re.search(r"<[^+]*>\s*$", comment):
+            tgt = base
+        funcs[cur].append((int(am.group(1), 16), ins, tgt))
+    return funcs
+
+
+def _classify(insns):
+    """Per instruction: 'P' stream DMA piece, 'F' saved-M0 DMA piece, 'V' other counted VM op,
+    'X' flat op, ('W', n) vmcnt wait, 'B' s_barrier, 'E' s_endpgm, or None."""
+    kinds = [None] * len(insns)
+    real = [k for k, (_, ins, _) in enumerate(insns) if ins.split()[0] != "s_nop"]
+    for j, k in enumerate(real):
+        ins = insns[k][1]
+        op = ins.split()[0]
+        if LDS_DMA.match(ins):
+            prev2 = insns[real[j - 2]][1] if j >= 2 else ""
+            after = insns[real[j + 1]][1] if j + 1 < len(real) else ""
+            saved = re.match(r"^s_mov_b32\s+s\d+\s*,\s*m0\s*$", prev2) and re.match(r"^s_mov_b32\s+m0\s*,\s*s\d+\s*$", after)
+            kinds[k] = "F" if saved else "P"
+        elif VM_OP.match(op):
+            kinds[k] = "V"
+        elif FLAT_OP.match(op):
+            kinds[k] = "X"
+        elif op == "s_waitcnt":
+            m = re.search(r"vmcnt\((\d+)\)", ins)
+            if m:
+                kinds[k] = ("W", int(m.group(1)))
+        elif op == "s_barrier":
+            kinds[k] = "B"
+        elif op == "s_endpgm":
+            kinds[k] = "E"
+    return kinds
+
+
+def check_vmcnt(insns, pieces_per_group, margins=None):
+    """Violations of the stream protocol (see above) in one kernel: [str].  margins (a dict), if
+    given, gets {barrier address: (smallest D - P - outstanding pieces over all states, wait count)}:
+    how many more pieces each publish could leave in flight."""
+    if not insns:
+        return []
+    kinds = _classify(insns)
+    addr_ix = {a: k for k, (a, _, _) in enumerate(insns)}
+    # basic blocks
+    leaders = {0}
+    for k, (_, ins, tgt) in enumerate(insns):
+        if BRANCH.match(ins) or kinds[k] == "E" or ins.startswith("s_setpc"):
+            if k + 1 < len(insns):
+                leaders.add(k + 1)
+            if tgt is not None:
+                if tgt not in addr_ix:
+                    return [f"{insns[k][0]:x}: branch target {tgt:x} is not an instruction"]
+                leaders.add(addr_ix[tgt])
+    starts = sorted(leaders)
+    block_of = {}
+    blocks = []
+    for bi, st in enumerate(starts):
+        end = starts[bi + 1] if bi + 1 < len(starts) else len(insns)
+        blocks.append((st, end))
+        block_of[st] = bi
+    succ = []
+    for st, end in blocks:
+        _, ins, tgt = insns[end - 1]
+        op = ins.split()[0]
+        s = []
+        if op == "s_branch":
+            s = [block_of[addr_ix[tgt]]]
+        elif op.startswith("s_cbranch"):
+            s = [block_of[addr_ix[tgt]]] + ([block_of[end]] if end in block_of else [])
+        elif op in ("s_endpgm",) or op.startswith("s_setpc"):
+            s = []
+        elif end in block_of:
+            s = [block_of[end]]
+        succ.append(s)
+    bad = []
+    seen = [set() for _ in blocks]
+    # state: (started, D = issued pieces - P * publishes, outstanding ops oldest first)
+    work = [(0, (False, 0, ()))]
+    seen[0].add((False, 0, ()))
+    while work:
+        bi, state = work.pop()
+        started, D, out = state
+        last_wait = None
+        st, end = blocks[bi]
+        for k in range(st, end):
+            kd = kinds[k]
+            if kd is None:
+                continue
+            where = f"{insns[k][0]:x}: {insns[k][1]}"
+            if kd == "P":
+                started, D, out = True, D + 1, (out + ("P",))[-63:]
+            elif kd in ("F", "V"):
+                out = (out + (kd,))[-63:]
+            elif kd == "X":
+                if "P" in out or "F" in out:
+                    bad.append(f"{where}: flat op while an LDS-DMA piece may be outstanding (flat retires out of order)")
+            elif kd[0] == "W":
+                n = last_wait = kd[1]
+                out = out[-n:] if n else ()
+            elif kd == "B" and started:
+                w = out.count("P")
+                if margins is not None:
+                    a = insns[k][0]
+                    old = margins.get(a, (1 << 30, None))[0]
+                    margins[a] = (min(old, D - pieces_per_group - w), last_wait)
+                if w > D - pieces_per_group:
+                    bad.append(f"{where}: barrier publishes a group whose pieces may be outstanding "
+                               f"({w} pieces may be in flight, at most {D - pieces_per_group} allowed)")
+                D -= pieces_per_group
+            elif kd == "E":
+                if "P" in out or "F" in out:
+                    bad.append(f"{where}: kernel ends with an LDS-DMA piece possibly outstanding")
+        if abs(D) > 64:
+            bad.append(f"{insns[end - 1][0]:x}: pieces issued and published diverge on some path (D = {D})")
+            continue
+        nxt = (started, D, out)
+        for sb in succ[bi]:
+            if nxt not in seen[sb]:
+                if len(seen[sb]) >= MAX_STATES:
+                    bad.append(f"{insns[blocks[sb][0]][0]:x}: too many states (the check does not converge)")
+                    return sorted(set(bad))
+                seen[sb].add(nxt)
+                work.append((sb, nxt))
+    return sorted(set(bad))
+
+
 def check(text, kernels=DEFAULT_KERNELS, streams=DEFAULT_STREAMS):
     """{kernel: violations} over the kernels matching `kernels` (regex), and the checked names."""
     report, checked = {}, []
+    addressed = _instructions(text)
     for name, insns in functions(text).items():
         if not re.search(kernels, name):
             continue
@@ -147,6 +329,10 @@ def check(text, kernels=DEFAULT_KERNELS, streams=DEFAULT_STREAMS):
         bad, pieces = check_function(insns)
         if pieces == 0 and re.search(streams, name):
             bad.append("no LDS-DMA piece found (the stream pattern changed: update this check)")
+        for pat, per in STREAM_PIECES:
+            if re.search(pat, name):
+                bad += check_vmcnt(addressed.get(name, []), per)
+                break
         if bad:
             report[name] = bad
     return report, checked

@@ -1,7 +1,20 @@
-"""The build-time M0 guard (scripts/check_isa.py, `make check-isa`): the LDS-DMA weight streams of
-mlp16_kernel and mlp_backward16_lds_kernel declare M0 clobbered, so nothing else in those kernels may
-read M0.  The check passes on the shipped libnerfmi.so and fails on the same disassembly with an M0
-reader inserted (explicit operand, implicit reader, a write the DMA does not consume)."""
+"""The build-time ISA guard (scripts/check_isa.py, `make check-isa`, run by __graft_entry__.build()).
+
+M0: the LDS-DMA weight streams of mlp16_kernel and mlp_backward16_lds_kernel declare M0 clobbered, so
+nothing else in those kernels may read M0.  The check passes on the shipped libnerfmi.so and fails on
+the same disassembly with an M0 reader inserted (explicit operand, implicit reader, a write the DMA does
+not consume).
+
+vmcnt: every publish of an LDS-DMA ring (the counted `s_waitcnt vmcnt(N)` + `s_barrier` of
+stream16.h, train.hip's bw_publish and wgrad_dma256_kernel) must leave in flight only pieces younger
+than the published chunk, on every path of the kernel's control-flow graph.  Shown on the shipped
+library (passes), on the shipped disassembly with one publish over-counted, a flat op in the window
+or the exit drain removed (fails), and on committed disassemblies of three builds
+(tests/golden/isa, scripts/make_isa_fixtures.py): the default, round 3's store-slack count (passes:
+within the window) and NERF16_WAIT_EXTRA=1 (fails at the group-boundary publishes).  On the GPU the
+passing builds train bit-identically to each other and the failing ones differ from run to run
+(profiles/r04/vmcnt_ab_overcount.log, scripts/vmcnt_ab.py): the check's boundary is the hardware's."""
+import gzip
 import os
 import re
 import shutil
@@ -15,12 +28,63 @@ sys.path.insert(0, os.path.join(REPO, "scripts"))
 import check_isa  # noqa: E402
 
 LIB = os.path.join(REPO, "depth-aware-shader-effects-for-nerf_amd", "libnerfmi.so")
-pytestmark = pytest.mark.skipif(not (os.path.exists(LIB) and shutil.which(os.path.join(check_isa.LLVM, "llvm-objdump"))),
-                                reason="needs the built library and ROCm's llvm-objdump")
+ISA_FIXTURES = os.path.join(REPO, "tests", "golden", "isa")
+
+
+@pytest.mark.parametrize("build,ok", [("head", True), ("r3slack", True), ("extra1", False)])
+def test_vmcnt_on_committed_builds(build, ok):
+    text = gzip.open(os.path.join(ISA_FIXTURES, f"{build}.txt.gz"), "rt").read()
+    report, checked = check_isa.check(text)
+    assert len(checked) == 2          # mlp16_kernel<true>, mlp_backward16_bound_kernel
+    if ok:
+        assert report == {}, report
+    else:
+        assert set(report) == set(checked), report
+        assert all(all("publishes" in b for b in v) for v in report.values()), report
+
+
+def _toy_kernel(n_loop_wait, n_pro_wait=4, drain=True):
+    """A hand-written stream kernel: chunks 0 and 1 (4 pieces each), publish 0, then a loop whose every
+    iteration issues the next chunk, stores (or not: a branch skips the store) and publishes."""
+    a = iter(range(0x100, 0x1000, 4))
+    L = ["0000000000000100 <k>:"]
+
+    def ins(t, tgt=None):
+        x = next(a)
+        L.append(f"\t{t} // {x:012X}: 0" + (f" <k+0x{tgt - 0x100:x}>" if tgt is not None else ""))
+        return x
+    for _ in range(8):
+        ins("s_mov_b32 m0, s4"); ins("global_load_lds_dwordx4 v1, s[2:3]")
+    ins(f"s_waitcnt vmcnt({n_pro_wait})"); ins("s_barrier")
+    top = ins("s_add_u32 s6, s6, 1")
+    for _ in range(4):
+        ins("s_mov_b32 m0, s4"); ins("global_load_lds_dwordx4 v1, s[2:3]")
+    L.append(None); br, bra = len(L) - 1, next(a)      # s_cbranch_execz over the store
+    ins("buffer_store_dword v2, v3, s[8:11], 0 offen")
+    join = ins("s_nop 0")
+    L[br] = f"\ts_cbranch_execz 1 // {bra:012X}: 0 <k+0x{join - 0x100:x}>"
+    ins(f"s_waitcnt vmcnt({n_loop_wait})"); ins("s_barrier")
+    ins("s_cbranch_scc1 0", tgt=top)
+    if drain:
+        ins("s_waitcnt vmcnt(0)")
+    ins("s_endpgm")
+    return check_isa._instructions("\n".join(L))["k"]
+
+
+def test_vmcnt_cfg_model():
+    """The toy kernel's exact counts pass; one more in the loop (the path that skips the store leaves
+    only the 4 pieces younger than the published chunk) or in the prologue is caught, and so is an
+    exit without the drain."""
+    assert check_isa.check_vmcnt(_toy_kernel(4), 4) == []
+    assert check_isa.check_vmcnt(_toy_kernel(5), 4)
+    assert check_isa.check_vmcnt(_toy_kernel(4, n_pro_wait=5), 4)
+    assert any("ends" in b for b in check_isa.check_vmcnt(_toy_kernel(4, drain=False), 4))
 
 
 @pytest.fixture(scope="module")
 def disasm():
+    if not (os.path.exists(LIB) and shutil.which(os.path.join(check_isa.LLVM, "llvm-objdump"))):
+        pytest.skip("needs the built library and ROCm's llvm-objdump")
     return check_isa.disassemble(LIB)
 
 
@@ -64,3 +128,55 @@ def test_unconsumed_m0_write_is_caught(disasm):
             break
     report, _ = check_isa.check("\n".join(lines))
     assert report
+
+
+# ---- counted vmcnt waits of the LDS-DMA streams (check_isa.check_vmcnt) ---------------------------
+def test_stream_kernels_are_checked(disasm):
+    report, checked = check_isa.check(disasm)
+    for k in ("mlp16_kernel<true>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel",
+              "wgrad_dma256_kernel<8>", "wgrad_dma256_kernel<5>"):
+        assert any(k in n for n in checked), k
+    assert report == {}, report
+
+
+def _publish_waits(text, kernel):
+    """Line indices of the counted waits (vmcnt(N), N > 0) that directly precede an s_barrier in `kernel`."""
+    lines = text.splitlines()
+    inside, out = False, []
+    for i, ln in enumerate(lines):
+        if re.match(r"^[0-9a-f]+ <.*>:$", ln):
+            inside = kernel in ln
+            continue
+        if inside and re.search(r"s_waitcnt vmcnt\(([1-9]\d*)\)", ln):
+            for x in lines[i + 1:i + 12]:            # the next barrier, before any other vmcnt wait
+                if "vmcnt" in x or re.match(r"^[0-9a-f]+ <", x):
+                    break
+                if "s_barrier" in x:
+                    out.append(i)
+                    break
+    return lines, out
+
+
+@pytest.mark.parametrize("kernel", ["mlp16_kernel<true>", "mlp_backward16_bound_kernel", "wgrad_dma256_kernel<8>"])
+def test_overcounted_publish_wait_is_caught(disasm, kernel):
+    """One publish wait counting one op more than issued after its chunk's pieces, in the ISA text."""
+    lines, waits = _publish_waits(disasm, kernel)
+    assert waits
+    i = waits[len(waits) // 2]
+    lines[i] = re.sub(r"vmcnt\((\d+)\)", lambda m: f"vmcnt({int(m.group(1)) + 8})", lines[i])
+    report, _ = check_isa.check("\n".join(lines))
+    assert any(kernel in n and any("publishes" in b for b in v) for n, v in report.items()), report
+
+
+def test_flat_op_in_flight_window_is_caught(disasm):
+    lines = disasm.splitlines()
+    inside = False
+    for i, ln in enumerate(lines):
+        if re.match(r"^[0-9a-f]+ <.*>:$", ln):
+            inside = "mlp16_kernel<true>" in ln
+        elif inside and "global_load_lds_dwordx4" in ln:
+            addr = re.search(r"//\s*([0-9A-F]+):", ln).group(1)
+            lines.insert(i + 1, f"\tflat_store_dword v[0:1], v2 // {addr}: 00000000")
+            break
+    report, _ = check_isa.check("\n".join(lines))
+    assert any("mlp16_kernel<true>" in n and any("flat op" in b for b in v) for n, v in report.items()), report
