@@ -204,14 +204,11 @@ def main():
     rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
     if rc is not None:
         sys.exit(rc)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        return dry_run(args, world, rank)
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dry_run(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
+    # under a launcher (WORLD_SIZE set, 1 included) the RCCL group exists and every collective below runs
+    world, rank, local, group = launch.init_ranks("nccl")
+    ranks = launch.rank_list(group)
     import nerfmi
     from nerfmi import _lib, cameras, frames
     nerfmi.set_mlp_arith(args.arith)
@@ -234,7 +231,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if group is not None:
         dist.barrier()
     cap = 4 * args.steps + 8
     torch.cuda.synchronize()
@@ -243,11 +240,11 @@ def main():
     for i in range(args.steps):
         step(args.warmup + i)
     torch.cuda.synchronize()
-    if world > 1:
+    if group is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launches = _lib.profile_mlp_end(cap)
-    if world > 1:
+    if group is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -279,6 +276,8 @@ def main():
             "value": total_rays / elapsed,
             "unit": "rays/s",
             "n_gpus": world,
+            "ranks": ranks,
+            "process_group": "nccl (RCCL)" if group is not None else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
@@ -315,7 +314,7 @@ def main():
                 return rgb
             line["cpu_baseline"], line["psnr_vs_reference_db"] = cpu_baseline(args.cpu_seconds, gpu_render)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if group is not None:
         dist.destroy_process_group()
 
 

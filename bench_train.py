@@ -152,16 +152,14 @@ def main():
     rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
     if rc is not None:
         sys.exit(rc)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        return dry_run(args, world, rank)
-    torch.cuda.set_device(local)
-    group = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        group = dist.group.WORLD
+        return dry_run(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
+    # under a launcher (WORLD_SIZE set, 1 included) the RCCL group exists: broadcast, gradient
+    # all-reduce, barriers and the max-over-ranks timing all run on the device
+    world, rank, local, group = launch.init_ranks("nccl")
+    if group is None:
+        torch.cuda.set_device(local)
+    ranks = launch.rank_list(group)
     import nerfmi
     from nerfmi import _lib
     from nerfmi.dataset import SyntheticNeRFDataset
@@ -236,7 +234,8 @@ def main():
         ach = M * flop / (ms * 1e-3) / 1e12
         traffic = pmc_traffic() if args.arith == "f16x3" else {}
         out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
-               "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps,
+               "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "ranks": ranks,
+               "process_group": "nccl (RCCL)" if group is not None else None, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None,
                "dtype": "fp32 (f16x3 split forward/data gradients, bf16x6 split weight gradients)"

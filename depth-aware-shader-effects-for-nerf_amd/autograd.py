@@ -31,7 +31,6 @@ from . import _lib
 from .models import APP_KEYS, STATE_KEYS, app_rows, state_tensors, uses_appearance
 from .ray_utils import draw_seed, linspace_table, rng_key_at
 
-_PACKED_T = {}
 # parameters that only the colour branch reads (models.py:141-160): no gradient when the loss does
 # not depend on rgb, as autograd leaves them (None, so torch.optim skips them)
 _COLOUR_KEYS = ("dir_linear.weight", "dir_linear.bias", "appearance_projection.weight",
@@ -62,22 +61,25 @@ def needs_grad(model, app, *inputs):
 
 def packed_pair(model):
     """(packed, packedT): the forward layout (render.packed_for) and the transposed weight fragments
-    the data-gradient chain reads, both re-packed when a parameter changes."""
+    the data-gradient chain reads, both re-packed when a parameter changes.  packedT is cached on the
+    module itself (it lives and dies with the model; the key holds each parameter's address and
+    version counter, so an in-place update or a new tensor re-packs)."""
     from .render import packed_for
     packed = packed_for(model)
     dev = packed.device
     sd = model.state_dict()
     key = (dev,) + tuple((sd[k].data_ptr(), sd[k]._version) for k in STATE_KEYS if k in sd)
-    hit = _PACKED_T.get(id(model))
+    hit = model.__dict__.get("_nerfmi_packedT")
     if hit is None or hit[0] != key:
         lib = _lib.load()
+        # (copies of host or non-fp32 parameters are freed after the pack is queued: the caching
+        # allocator reuses their memory only for work queued after it on this stream)
         ts = [t.detach().to(dev, torch.float32).contiguous() for t in state_tensors(sd, dev)]
         arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in ts])
         packedT = torch.empty(lib.nerf_packed_transposed_floats(), device=dev)
         _lib.check(lib.nerf_pack_weights_transposed(arr, _lib.ptr(packedT), _lib.stream()),
                    "nerf_pack_weights_transposed")
-        _PACKED_T[id(model)] = (key, packedT, ts)
-        hit = _PACKED_T[id(model)]
+        hit = model.__dict__["_nerfmi_packedT"] = (key, packedT)
     return packed, hit[1]
 
 

@@ -25,9 +25,11 @@ def shard_range(n_rays, world, rank):
 
 
 def _world(group):
+    """(world, rank, collective): collective is True whenever a process group exists, world 1
+    included, so the all-gather runs on the device under any launcher (tests/test_gpu_rccl.py)."""
     if dist.is_available() and dist.is_initialized():
-        return dist.get_world_size(group), dist.get_rank(group)
-    return 1, 0
+        return dist.get_world_size(group), dist.get_rank(group), True
+    return 1, 0, False
 
 
 def shard_rays(ray_fn, H, W, n_frames, start, end):
@@ -59,6 +61,7 @@ def _render_shard(ray_fn, render_fn, H, W, n_frames, start, end, buf):
         buf[: end - start, 3:] = depth.reshape(-1, 1).to(buf.device)
 
 
+@torch.no_grad()
 def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=None, virtual_shards=None):
     """Render n_frames HxW frames over the ranks of `group`.
 
@@ -69,9 +72,11 @@ def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=
     virtual_shards=G (one process only): render the G shards G ranks would render, one after the
     other, and reassemble them as the all-gather would (the 1-GPU "G virtual shards"
     check of the sharding and reassembly of a G-GPU run).
-    Returns (rgb (n_frames,H,W,3), depth (n_frames,H,W)) on every rank.
+    Returns (rgb (n_frames,H,W,3), depth (n_frames,H,W)) on every rank.  Inference only (no autograd
+    graph: the outputs are copied into the reassembly buffer, as the reference renders its frames
+    under torch.no_grad(), run.py:217).
     """
-    world, rank = _world(group)
+    world, rank, collective = _world(group)
     total = n_frames * H * W
     if virtual_shards is not None:
         if world != 1:
@@ -86,7 +91,7 @@ def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=
         start, end, per = shard_range(total, world, rank)
         buf = torch.zeros(per, 4, device=device)
         _render_shard(ray_fn, render_fn, H, W, n_frames, start, end, buf)
-        if world > 1:
+        if collective:
             out = torch.empty(world * per, 4, device=buf.device)
             dist.all_gather_into_tensor(out, buf, group=group)
         else:
@@ -95,6 +100,7 @@ def render_frames_sharded(ray_fn, render_fn, H, W, n_frames, group=None, device=
     return frames[..., :3], frames[..., 3]
 
 
+@torch.no_grad()
 def render_path_frames(model, poses, H, W, focal, near, far, n_samples, n_importance=0, appearance_embedding=None,
                        perturb=False, hierarchical=False, seed=0, group=None, timing=None, virtual_shards=None):
     """render_frames_sharded with nerfmi's HIP get_rays / render_rays (one list entry per frame:

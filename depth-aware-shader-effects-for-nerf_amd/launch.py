@@ -41,3 +41,32 @@ def world_or_launch(gpus, script, argv, check_devices=True):
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", script] + list(argv)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     return subprocess.call(cmd, env=env)
+
+
+def init_ranks(backend="nccl"):
+    """(world, rank, local_rank, group) of this process.  Under a launcher (WORLD_SIZE set, world 1
+    included) the device is set to LOCAL_RANK and the process group is initialised on `backend`
+    ("nccl" = RCCL over xGMI on ROCm), so the collectives of the benches and the CLI run on the
+    device even on one GPU; a plain `python bench.py` has no group (None) and runs no collective."""
+    import torch
+    import torch.distributed as dist
+    if os.environ.get("WORLD_SIZE") is None:
+        return 1, 0, 0, None
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return world, rank, local, dist.group.WORLD
+
+
+def rank_list(group):
+    """Every rank's global rank as the group sees it (all_gather_object): [0] alone."""
+    if group is None:
+        return [0]
+    import torch.distributed as dist
+    got = [None] * dist.get_world_size(group)
+    dist.all_gather_object(got, dist.get_rank(), group=group)
+    return got

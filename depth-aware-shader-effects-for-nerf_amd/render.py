@@ -29,7 +29,8 @@ the reference-compat call (coarse; hierarchical, staged and timing unset) runs t
 kernels instead (autograd.py): rgb_map and depth_map carry a grad_fn whose backward is the
 composite backward + MLP data-gradient chain + weight-gradient reductions of csrc/train.hip, as
 the reference's training loop needs (src/train.py:77-92).  The H1 hierarchical pass has no
-reference training semantics (render.py:83-86 is a stub) and always renders without a graph.
+reference training semantics (render.py:83-86 is a stub): with gradients enabled and a trainable
+model it raises (RuntimeError naming hierarchical=True) instead of silently returning no graph.
 """
 import torch
 
@@ -37,7 +38,6 @@ from . import _lib
 from .models import STATE_KEYS, app_rows, pack_params, run_mlp, state_tensors, uses_appearance
 from .ray_utils import draw_seed, linspace_table, rng_key_at
 
-_FOREIGN = {}
 _IMPORTANCE_KEY = 0x5DEECE66D     # the inverse-CDF stream's key: seed ^ this (include/nerfmi.h)
 
 
@@ -48,18 +48,25 @@ def packed_for(model):
         return model.packed_weights()
     dev = _lib.device()
     sd = model.state_dict()
-    key = (id(model), dev) + tuple((sd[k].data_ptr(), sd[k]._version) for k in STATE_KEYS if k in sd)
-    if _FOREIGN.get(id(model), (None,))[0] != key:
-        _FOREIGN[id(model)] = (key, pack_params(state_tensors(sd, dev), dev))
-    return _FOREIGN[id(model)][1]
+    key = (dev,) + tuple((sd[k].data_ptr(), sd[k]._version) for k in STATE_KEYS if k in sd)
+    hit = model.__dict__.get("_nerfmi_packed")          # cached on the module: lives and dies with it
+    if hit is None or hit[0] != key:
+        hit = model.__dict__["_nerfmi_packed"] = (key, pack_params(state_tensors(sd, dev), dev))
+    return hit[1]
 
 
 def volume_render(model, rays_o, rays_d, near, far, n_samples, n_importance, appearance_embedding=None,
                   background_color=None, perturb=True, *, hierarchical=False, t_rand=None, u_rand=None,
                   seed=None, ray_offset=0, timing=None, staged=False, reuse_coarse=True):
     from . import autograd
-    if not (hierarchical or staged or timing is not None) and \
-            autograd.needs_grad(model, appearance_embedding if uses_appearance(model) else None, rays_o, rays_d):
+    if autograd.needs_grad(model, appearance_embedding if uses_appearance(model) else None, rays_o, rays_d):
+        if hierarchical or staged or timing is not None:
+            what = "hierarchical=True" if hierarchical else ("staged=True" if staged else "timing=")
+            raise RuntimeError(
+                f"nerfmi.volume_render({what}) has no differentiable path: the reference's fine pass is a stub "
+                f"with no training semantics (src/render.py:83-86) and the staged/timed paths are inference "
+                f"instrumentation.  Render under torch.no_grad() (as the reference's run.py:217 does) or with "
+                f"parameters that do not require grad; the coarse call (hierarchical=False) is differentiable.")
         return autograd.volume_render_grad(model, rays_o, rays_d, near, far, n_samples, appearance_embedding,
                                            perturb, t_rand=t_rand, seed=seed, ray_offset=ray_offset)
     dev = _lib.device()

@@ -312,10 +312,9 @@ def broadcast_state(tensors, group):
     if group is None:
         return
     import torch.distributed as dist
-    if dist.get_world_size(group) > 1:
-        src = dist.get_global_rank(group, 0)
-        for t in tensors:
-            dist.broadcast(t, src=src, group=group)
+    src = dist.get_global_rank(group, 0)
+    for t in tensors:
+        dist.broadcast(t, src=src, group=group)
 
 
 def average_gradients(flat_grad, group):
@@ -327,8 +326,8 @@ def average_gradients(flat_grad, group):
         return
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    dist.all_reduce(flat_grad, group=group)     # (world 1 included: the collective runs whenever a group exists)
     if world > 1:
-        dist.all_reduce(flat_grad, group=group)
         flat_grad.div_(world)
 
 

@@ -102,6 +102,7 @@ class SceneInfo:
         self.appearance_embeddings = torch.randn(n_images, config.appearance_dim)
 
 
+@torch.no_grad()                                   # the reference renders its path under no_grad (run.py:217)
 def render_path(model, scene, config, output_dir, num_frames=120, quality='high', width=800, height=800,
                 start_frame=0, end_frame=None, save_depth=False, raw_output=False, camera_path='circle',
                 spiral_loops=2.0, height_range=(-0.5, 0.5), hierarchical=False, n_importance=None, chunk=0,
@@ -222,21 +223,20 @@ def main(argv=None):
             print(f"nerfmi: effect {shader!r} is not on the GPU path; available: {sorted(PostProcessor().effects)}")
             return 2
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world > 1:
-        local = int(os.environ.get('LOCAL_RANK', '0'))
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from nerfmi import launch
+    # under a launcher (WORLD_SIZE set, 1 included): one rank per GPU, RCCL group for the frame
+    # all-gather / gradient all-reduce
+    world, rank, _, group = launch.init_ranks('nccl')
     if args.mode == 'train':                                           # run.py:326-347
         from nerfmi.dataset import make_dataset
         from nerfmi.train import train_nerf
-        np.random.seed(args.seed + (dist.get_rank() if world > 1 else 0))
+        np.random.seed(args.seed + rank)
         dataset = make_dataset(config)
         model_dimension_check(config)                                  # run.py:327-345
         torch.manual_seed(args.random_init or 0)
         model = train_nerf(config, dataset, save_dir=args.save_dir, num_iterations=args.iterations,   # run.py:347
-                           group=dist.group.WORLD if world > 1 else None)
-        if world > 1:
+                           group=group)
+        if group is not None:
             dist.destroy_process_group()
         return 0
     checkpoint = args.checkpoint
@@ -265,7 +265,7 @@ def main(argv=None):
                     spiral_loops=args.spiral_loops, height_range=args.height_range,
                     hierarchical=args.hierarchical, n_importance=args.n_importance, chunk=args.chunk,
                     seed=args.seed, shader=shader)
-    if world > 1:
+    if group is not None:
         dist.destroy_process_group()
     return 0
 

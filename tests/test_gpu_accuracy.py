@@ -154,21 +154,54 @@ def test_h1_render_vs_float64(which, ref_state, app_vec, trained_state, arith):
     check_no_worse_than_cpu(depth.cpu(), d32, d64, f"{which}/{arith} depth")
 
 
+def gpu_relu_masks(model, x, d, app):
+    """The ten ReLU branches (models.py:128-150: trunk layers 0-7, density, dir_linear) the GPU's forward
+    with saves took on these points, read from its saved activations (ReLU output > 0, the mask the
+    backward applies): the same C calls as nerfmi.autograd._MLPFn, under the arithmetic in force."""
+    from nerfmi import _lib
+    from nerfmi.autograd import packed_pair
+    lib, s, P = _lib.load(), _lib.stream(), _lib.ptr
+    packed, _ = packed_pair(model)
+    M, dev = x.shape[0], x.device
+    appd = app.reshape(1, 32).to(dev).contiguous()
+    feat, encd = torch.empty(M, 256, device=dev), torch.empty(M, 32, device=dev)
+    z = torch.zeros(M, 1, device=dev)
+    rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
+    MT = _lib.tile_rows(M)
+    save = torch.empty(MT, _lib.SAVE_ROW, device=dev)
+    masks = torch.empty(M, _lib.MASK_ROW, dtype=torch.int32, device=dev) if _lib.get_mlp_arith() == "f16x3" else None
+    _lib.check(lib.nerf_ray_features_train(P(packed), P(d), M, P(appd), 1, P(feat), P(encd), s), "features")
+    _lib.check(lib.nerf_mlp_forward_train(P(packed), P(x), P(d), P(z), M, 1, P(feat), P(encd), P(rgb), P(sigma),
+                                          P(save), P(masks), s), "mlp_forward_train")
+    # tile-major rows (layout.h tile_off): [block][feature group][sample in block][feature % 8]
+    rows = save.view(MT // 32, _lib.SAVE_ROW // 8, 32, 8).permute(0, 2, 1, 3).reshape(MT, _lib.SAVE_ROW)[:M].cpu()
+    h_at = [l * 256 if l < 4 else 1024 + 64 + (l - 4) * 256 for l in range(8)]        # layout.h save_h
+    out = [rows[:, a:a + 256] > 0 for a in h_at]
+    out.append((sigma.cpu() > 0).reshape(M, 1))
+    out.append(rows[:, 2144:2144 + 128] > 0)                                          # kSaveRDir
+    return out
+
+
 @pytest.mark.parametrize("which", ["trained", "adversarial"])
 def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
     """Every parameter gradient of NeRF.forward (the training kernels through autograd: forward with
     saves, data-gradient chain, weight-gradient GEMMs) against float64 autograd, on trained and
-    adversarial weights.  The f16x3 data gradient splits each layer's gradient at a scale taken from
-    a pack-time bound (max row-L1 norm of W^T, csrc/train.hip mlp_backward16_bound_kernel), which the
-    adversarial rows loosen by up to 2^7: the GPU's per-tensor error must stay within twice the fp32
-    CPU autograd's own error against float64 (+1e-6 rel-L2 for tensors the two both get to ~eps).
-    One exception, measured: the f16x3 FORWARD on the adversarial weights, whose split scales come from
-    the same kind of loose bound (R_L max|a| + B_L, mlp16.hip), carries up to 4x the CPU's error
-    (test_forward above); the gradient of pts_linears.4.bias inherits it (rel-L2 2.73e-6 against the
-    CPU's 3.8e-7, identical to 3 digits whether the data gradient's scale is the bound or the exact row
-    maximum, so it is not the backward's), so that case is held to 8x.  The saturated colour head of
-    the adversarial model (sigmoid = 1 in fp32) makes the colour-branch tensors ~100 % off float64 in
-    both fp32 evaluations alike."""
+    adversarial weights.  The reference gradient of an evaluation is float64 autograd on the SAME
+    piecewise-linear branch that evaluation took: its own ReLU masks (the GPU's from its saved
+    activations, the CPU fp32 autograd's from its pre-activations).  A point whose pre-activation sits
+    within rounding of a ReLU kink then costs each evaluation only its rounding, not a jump between two
+    linear pieces (round 3's trained fixtures put one such point at ~1,000x the CPU's error, on
+    whichever tensor the kink fed).  The GPU's per-tensor error must stay within twice the fp32 CPU
+    autograd's own (+1e-6 rel-L2 for tensors the two both get to ~eps).  The f16x3 data gradient splits
+    each layer's gradient at a scale taken from a pack-time bound (csrc/train.hip
+    mlp_backward16_bound_kernel), which the adversarial rows loosen by up to 2^7.  One exception,
+    measured: the f16x3 FORWARD on the adversarial weights (split scales from the same kind of loose
+    bound, R_L max|a| + B_L, mlp16.hip) carries up to 4x the CPU's error (test_forward above), and the
+    gradient of pts_linears.4.bias inherits it (rel-L2 2.7e-6 against the CPU's 3.8e-7, the same whether
+    the data gradient's scale is the bound or the exact row maximum, so it is not the backward's): that
+    one tensor of that one case is held to 8x.  The saturated colour head of the adversarial model
+    (sigmoid = 1 in fp32) makes the colour-branch tensors ~100 % off float64 in both fp32 evaluations
+    alike."""
     import nerfmi
     st, app = weights(which, ref_state, app_vec, trained_state)
     model = nerfmi.NeRF(nerfmi.Config())
@@ -181,24 +214,35 @@ def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
     g_rgb, g_sig = torch.randn(M, 3, generator=g), torch.randn(M, 1, generator=g)
     rgb, sigma = model(x.cuda(), d.cuda(), app.cuda())
     ((rgb * g_rgb.cuda()).sum() + (sigma * g_sig.cuda()).sum()).backward()
+    with torch.no_grad():
+        m_gpu = gpu_relu_masks(model, x.cuda(), d.cuda(), app)
 
-    def ref_grads(dtype):
+    def ref_grads(dtype, masks=None, record=None):
         sd = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in st.items()}   # fresh leaves
+
+        def relu(pre, i):
+            if record is not None:
+                record.append(pre.detach() > 0)
+            return torch.relu(pre) if masks is None else pre * masks[i].to(dtype)
         with torch.enable_grad():
-            r, s = O.nerf_forward(sd, x.to(dtype), d.to(dtype), app.to(dtype))
+            r, s = O.nerf_forward(sd, x.to(dtype), d.to(dtype), app.to(dtype), relu=relu)
             ((r * g_rgb.to(dtype)).sum() + (s * g_sig.to(dtype)).sum()).backward()
         return {k: v.grad.double() for k, v in sd.items()}
 
-    g32, g64 = ref_grads(torch.float32), ref_grads(torch.float64)
+    m_cpu = []
+    g32 = ref_grads(torch.float32, record=m_cpu)
+    g64_cpu, g64_gpu = ref_grads(torch.float64, masks=m_cpu), ref_grads(torch.float64, masks=m_gpu)
+    flips = sum(int((a != b).sum()) for a, b in zip(m_cpu, m_gpu))
 
     def rel(a, b):
         return float((a - b).norm() / (b.norm() + 1e-300))
 
     worst = []
     for k, p in model.named_parameters():
-        e_gpu, e_cpu = rel(p.grad.cpu().double(), g64[k]), rel(g32[k], g64[k])
-        f = 8.0 if (which == "adversarial" and arith == "f16x3") else 2.0
+        e_gpu, e_cpu = rel(p.grad.cpu().double(), g64_gpu[k]), rel(g32[k], g64_cpu[k])
+        f = 8.0 if (which == "adversarial" and arith == "f16x3" and k == "pts_linears.4.bias") else 2.0
         worst.append((e_gpu / (f * e_cpu + 1e-6), k, e_gpu, e_cpu))
         assert e_gpu <= f * e_cpu + 1e-6, (which, arith, k, e_gpu, e_cpu)
     worst.sort(reverse=True)
-    print(f"{which}/{arith}: worst gradient tensors (ratio to the bound, key, gpu rel-L2, cpu rel-L2): {worst[:3]}")
+    print(f"{which}/{arith}: {flips} ReLU branches differ between the GPU and the CPU; worst gradient tensors "
+          f"(ratio to the bound, key, gpu rel-L2, cpu rel-L2): {worst[:3]}")

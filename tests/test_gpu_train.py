@@ -42,6 +42,19 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
+def close_unless_zero_gradient(a, b, rtol, name, rel_g_max=1e-3):
+    """Sampled gradient entries a against the reference's b: every entry within rtol, except where the
+    reference gradient is ~0, i.e. at most rel_g_max of the largest (cancellation, where the rounding of
+    two evaluations decides sign and size: _params_close's rule for the parameters).  The largest is
+    taken over the sampled entries, which can only make the exception rarer."""
+    a, b = np.asarray(a, np.float64).ravel(), np.asarray(b, np.float64).ravel()
+    scale = np.abs(b).max() + 1e-30
+    off = np.abs(a - b) > rtol * np.abs(b) + 1e-4 * rtol * scale
+    rel = np.abs(b) / scale
+    assert np.all(rel[off] <= rel_g_max), (name, int(off.sum()), float(rel[off].max()))
+    return rel
+
+
 def mostly_close(a, b, rtol=1e-3, frac=0.999):
     a, b = np.asarray(a, np.float64).ravel(), np.asarray(b, np.float64).ravel()
     scale = np.abs(b).max() + 1e-30
@@ -476,9 +489,8 @@ def test_trainer_step_matches_reference_f7(golden, golden_meta, ref_state):
         prm = tr.view(tr.flat, i).detach().cpu()
         if f"idx/{name}" in f7:
             idx = torch.from_numpy(f7[f"idx/{name}"])
-            ok, frac = mostly_close(g.reshape(-1)[idx].numpy(), f7[f"grad/{name}"], rtol=2e-3, frac=0.95)
-            assert ok, (name, frac)
-            _params_close(prm.reshape(-1)[idx].numpy(), f7[f"param/{name}"], 1, name, frac=0.95)
+            rel = close_unless_zero_gradient(g.reshape(-1)[idx].numpy(), f7[f"grad/{name}"], 2e-3, name)
+            _params_close(prm.reshape(-1)[idx].numpy(), f7[f"param/{name}"], 1, name, frac=None, rel_g=rel)
         else:
             assert rel_l2(g.numpy(), f7[f"grad/{name}"]) < 5e-4, name
             ga = np.abs(f7[f"grad/{name}"].astype(np.float64))
@@ -495,6 +507,7 @@ def test_trainer_matches_oracle_over_steps(ref_state):
     opt = None
     focal = cameras.synthetic_focal(800)
     g = torch.Generator().manual_seed(21)
+    rel_g = {}                        # per entry: the smallest |reference gradient| / tensor max over the steps
     for step in range(3):
         c2w = cameras.frame_c2w("chair", "circle", 10 * step, 120).float()
         o_all, d_all = get_rays(800, 800, focal, c2w.to(tr.dev))
@@ -510,6 +523,9 @@ def test_trainer_matches_oracle_over_steps(ref_state):
         for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
             got = tr.view(tr.grad, i).detach().cpu().numpy()
             assert rel_l2(got, grads_o[n].numpy()) < 5e-4, (step, n, rel_l2(got, grads_o[n].numpy()))
+            ga = np.abs(grads_o[n].double().numpy())
+            r = ga / max(ga.max(), 1e-30)
+            rel_g[n] = r if n not in rel_g else np.minimum(rel_g[n], r)
         tr.optimizer_step()
     torch.cuda.synchronize()
     names = list(O.STATE_KEYS) + ["appearance_embeddings"]
@@ -517,10 +533,9 @@ def test_trainer_matches_oracle_over_steps(ref_state):
     for i, n in enumerate(names):
         got = tr.view(tr.flat, i).detach().cpu().numpy()
         exp = params[n].detach().numpy()
-        # after 3 steps a sign flip at one step feeds the later steps' gradients, so which entries
-        # differ is no longer local (the one-step F7 test checks the flip criterion entry by
-        # entry): up to 2% of entries may differ, each within the 2*lr*steps bound
-        _params_close(got, exp, 3, n, frac=0.98)
+        # an entry may differ (within the 2*lr*steps bound) only where its reference gradient was ~0
+        # at one of the steps: there Adam's first moves take the sign of the rounding
+        _params_close(got, exp, 3, n, frac=None, rel_g=rel_g[n])
 
 
 def test_training_reduces_loss_on_teacher_scene():
@@ -626,4 +641,6 @@ def test_no_appearance_model_trains_like_the_oracle(noapp_state):
     sd = tr.optimizer_state_dict()
     assert len(sd["param_groups"][0]["params"]) == 22 and sorted(sd["state"]) == list(range(22))
     for k in noapp_state:
-        _params_close(model.state_dict()[k].cpu().numpy(), st[k].detach().numpy(), 1, k, frac=0.99)
+        ga = np.abs(grads_o[k].double().numpy())
+        _params_close(model.state_dict()[k].cpu().numpy(), st[k].detach().numpy(), 1, k, frac=None,
+                      rel_g=ga / max(ga.max(), 1e-30))
