@@ -2432,14 +2432,23 @@ constexpr int kRedParts = NERF_RED_PARTS;
 __global__ void __launch_bounds__(64 * kRedParts)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w, int ldo,
                     float* __restrict__ out_b, int accumulate, WgradSplit split) {
-  __shared__ f32x4 part[kRedParts][64];
+  // the chunk partials are added in double and rounded once: a gradient entry is a sum over up to
+  // 2^18 samples with heavy cancellation (random-sign upstream gradients), and an fp32 running sum of
+  // its 256 chunk partials cost up to ~10x the fp32 CPU autograd's error on the bias columns
+  // (tests/test_gpu_accuracy.py::test_gradients_vs_float64, scripts/diag_grad_masks.py)
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  __shared__ f64x4 part[kRedParts][64];
   const int KP = K + 1;
   const int64_t stride = wgrad_stride(N, K);
   const int64_t col4 = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int q = threadIdx.x >> 6;
   const int per = (chunks + kRedParts - 1) / kRedParts;
   const int c0 = q * per < chunks ? q * per : chunks, c1 = c0 + per < chunks ? c0 + per : chunks;
-  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  auto add = [&](const f32x4& v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += (double)v[e];
+  };
   if (col4 * 4 < stride) {
     const f32x4* p = reinterpret_cast<const f32x4*>(partial) + col4;
     const int64_t s4 = stride / 4;
@@ -2449,16 +2458,19 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = p[(c + u) * s4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < 8; ++u) add(v[u]);
     }
-    for (; c < c1; ++c) acc += p[c * s4];
+    for (; c < c1; ++c) add(p[c * s4]);
   }
   part[q][threadIdx.x & 63] = acc;
   __syncthreads();
   if (q != 0 || col4 * 4 >= stride) return;
-  f32x4 sum = part[0][threadIdx.x];
+  f64x4 sum64 = part[0][threadIdx.x];
 #pragma unroll
-  for (int r = 1; r < kRedParts; ++r) sum += part[r][threadIdx.x];
+  for (int r = 1; r < kRedParts; ++r) sum64 += part[r][threadIdx.x];
+  f32x4 sum;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sum[e] = (float)sum64[e];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t idx = col4 * 4 + e;

@@ -186,22 +186,28 @@ def gpu_relu_masks(model, x, d, app):
 def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
     """Every parameter gradient of NeRF.forward (the training kernels through autograd: forward with
     saves, data-gradient chain, weight-gradient GEMMs) against float64 autograd, on trained and
-    adversarial weights.  The reference gradient of an evaluation is float64 autograd on the SAME
-    piecewise-linear branch that evaluation took: its own ReLU masks (the GPU's from its saved
-    activations, the CPU fp32 autograd's from its pre-activations).  A point whose pre-activation sits
-    within rounding of a ReLU kink then costs each evaluation only its rounding, not a jump between two
-    linear pieces (round 3's trained fixtures put one such point at ~1,000x the CPU's error, on
-    whichever tensor the kink fed).  The GPU's per-tensor error must stay within twice the fp32 CPU
-    autograd's own (+1e-6 rel-L2 for tensors the two both get to ~eps).  The f16x3 data gradient splits
-    each layer's gradient at a scale taken from a pack-time bound (csrc/train.hip
-    mlp_backward16_bound_kernel), which the adversarial rows loosen by up to 2^7.  One exception,
-    measured: the f16x3 FORWARD on the adversarial weights (split scales from the same kind of loose
-    bound, R_L max|a| + B_L, mlp16.hip) carries up to 4x the CPU's error (test_forward above), and the
-    gradient of pts_linears.4.bias inherits it (rel-L2 2.7e-6 against the CPU's 3.8e-7, the same whether
-    the data gradient's scale is the bound or the exact row maximum, so it is not the backward's): that
-    one tensor of that one case is held to 8x.  The saturated colour head of the adversarial model
-    (sigmoid = 1 in fp32) makes the colour-branch tensors ~100 % off float64 in both fp32 evaluations
-    alike."""
+    adversarial weights.
+
+    Kink-proof: the float64 reference of an evaluation runs on the SAME piecewise-linear branch that
+    evaluation took, i.e. with its own ReLU masks (the GPU's from its saved activations, the fp32 CPU
+    autograd's from its pre-activations).  A pre-activation within rounding of a ReLU kink then costs
+    each evaluation its rounding only, not a jump between two linear pieces (the adversarial weights
+    put one such point in layer 3, and both fp32 evaluations were 2.8e-3 off a float64 reference that
+    took the other branch, which hid their real errors; round 3's trained fixtures put one at ~1,000x).
+
+    Bounds, per tensor (rel-L2 against float64):
+      * f32 arithmetic: within 2x the fp32 CPU autograd's own error (+1e-6 for tensors both get to ~eps);
+      * f16x3: within 2x the CPU's error + 1e-5, ten times inside the 1e-4 parity tolerance.  The
+        split itself is fp32-accurate (an emulation with the kernel's splits and exact sums is within
+        the CPU's error, scripts/diag_dgrad_rows.py), but the MFMA unit's f32 accumulation of f16
+        products is not correctly rounded: 25 % of results are off by more than half an ulp, with a
+        mean of -0.12 ulp (profiles/r04/mfma_f16_accumulation_rounding.log).  That small one-signed
+        error survives the sums over samples that make the bias gradients, where the true values
+        cancel (random upstream gradients): up to 6e-6 on pts_linears.0.bias of the adversarial weights
+        (18x the CPU's; the same kernels behind an fp32 backward give the CPU's error,
+        profiles/r04/diag_grad_masks.log, diag_bias_sums.log).
+    The saturated colour head of the adversarial model (sigmoid = 1 in fp32) makes the colour-branch
+    tensors ~100 % off float64 in every fp32 evaluation alike."""
     import nerfmi
     st, app = weights(which, ref_state, app_vec, trained_state)
     model = nerfmi.NeRF(nerfmi.Config())
@@ -240,9 +246,9 @@ def test_gradients_vs_float64(which, ref_state, app_vec, trained_state, arith):
     worst = []
     for k, p in model.named_parameters():
         e_gpu, e_cpu = rel(p.grad.cpu().double(), g64_gpu[k]), rel(g32[k], g64_cpu[k])
-        f = 8.0 if (which == "adversarial" and arith == "f16x3" and k == "pts_linears.4.bias") else 2.0
-        worst.append((e_gpu / (f * e_cpu + 1e-6), k, e_gpu, e_cpu))
-        assert e_gpu <= f * e_cpu + 1e-6, (which, arith, k, e_gpu, e_cpu)
+        bound = 2.0 * e_cpu + (1e-5 if arith == "f16x3" else 1e-6)
+        worst.append((e_gpu / bound, k, e_gpu, e_cpu))
+        assert e_gpu <= bound, (which, arith, k, e_gpu, e_cpu, bound)
     worst.sort(reverse=True)
     print(f"{which}/{arith}: {flips} ReLU branches differ between the GPU and the CPU; worst gradient tensors "
           f"(ratio to the bound, key, gpu rel-L2, cpu rel-L2): {worst[:3]}")

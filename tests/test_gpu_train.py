@@ -8,6 +8,13 @@ agree to ~1e-5 relative in L2; a ReLU whose
 pre-activation sits within fp32 rounding of 0 can flip its mask between fp32 and fp64 and
 perturb single entries, so per-layer checks bound the relative L2 error (2e-4) and require
 >= 99.9% of entries within rtol 1e-3 rather than demanding every entry.
+
+Against the reference's own steps (fixture F7) and the oracle's multi-step training, gradients and
+parameters are held to a float64 run of the same step(s): the GPU's deviation from float64 is no
+larger than the reference's fp32 CPU deviation (grads_no_worse_than_reference,
+params_no_worse_than_reference).  A fraction-of-entries tolerance would let a real error hide in the
+allowed fraction; this lets only the entries the reference itself cannot pin down (a ReLU kink in
+the float64 run, a gradient cancelling to ~0 whose sign decides Adam's first move) differ.
 """
 import ctypes
 
@@ -42,17 +49,44 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def close_unless_zero_gradient(a, b, rtol, name, rel_g_max=1e-3):
-    """Sampled gradient entries a against the reference's b: every entry within rtol, except where the
-    reference gradient is ~0, i.e. at most rel_g_max of the largest (cancellation, where the rounding of
-    two evaluations decides sign and size: _params_close's rule for the parameters).  The largest is
-    taken over the sampled entries, which can only make the exception rarer."""
-    a, b = np.asarray(a, np.float64).ravel(), np.asarray(b, np.float64).ravel()
-    scale = np.abs(b).max() + 1e-30
-    off = np.abs(a - b) > rtol * np.abs(b) + 1e-4 * rtol * scale
-    rel = np.abs(b) / scale
-    assert np.all(rel[off] <= rel_g_max), (name, int(off.sum()), float(rel[off].max()))
-    return rel
+def f7_float64(ref_state, f7, meta):
+    """Fixture F7's training step (one reference step, src/train.py:77-92) run by the oracle in
+    float64 from the same weights, table, rays and jitter: (gradients, updated parameters), keyed by
+    F7's names.  F7 is the reference's own fp32 CPU step, so it and the GPU can both be measured
+    against this float64 truth."""
+    st = {k: v.double().clone() for k, v in ref_state.items()}
+    torch.manual_seed(1)
+    table = torch.randn(100, 32).double()
+    t_rand = seeded_uniform(meta["seed_t_rand"], (256, 64), meta["t_rand_sha256"])
+    o, d, tgt = (torch.from_numpy(f7[k]).double() for k in ("o", "d", "target"))
+    _, _, g64, _ = O.train_step(st, table, 0, o, d, tgt, 2.0, 6.0, 64, t_rand.double(), lr=meta["lr"])
+    params = dict(st, appearance_embeddings=table)
+    return ({k: v.detach().numpy() for k, v in g64.items()},
+            {k: v.detach().numpy() for k, v in params.items()})
+
+
+def grads_no_worse_than_reference(got, ref, f64, name, factor=1.5):
+    """Gradient entries (F7's sampled ones): the GPU's deviation from float64 is no larger than the
+    reference's own fp32 step's, in max, p99.9 and median, each relative to the tensor's largest
+    float64 entry (per-entry relative errors are meaningless at entries that cancel to ~0)."""
+    got, ref, f64 = (np.asarray(t, np.float64).ravel() for t in (got, ref, f64))
+    sc = np.abs(f64).max() + 1e-300
+    eg, er = np.abs(got - f64) / sc, np.abs(ref - f64) / sc
+    for stat, f in (("max", np.max), ("p99.9", lambda v: np.quantile(v, 0.999)), ("median", np.median)):
+        assert f(eg) <= factor * f(er) + 1e-9, (name, stat, float(f(eg)), float(f(er)))
+
+
+def params_no_worse_than_reference(got, ref, f64, name, tol=2e-6):
+    """Parameters after Adam steps: Adam's first moves are +-lr by the sign of the gradient, so an entry
+    whose gradient cancels to ~0 lands +-lr apart between any two fp32 evaluations, and a flip feeds
+    the later steps.  Held to the float64 trajectory like the reference's fp32 CPU steps: no more entries
+    off it by > tol than the reference (x1.25 + 4), and the largest deviation within twice the
+    reference's (+ tol)."""
+    got, ref, f64 = (np.asarray(t, np.float64).ravel() for t in (got, ref, f64))
+    og, orf = int((np.abs(got - f64) > tol).sum()), int((np.abs(ref - f64) > tol).sum())
+    assert og <= 1.25 * orf + 4, (name, "entries off the float64 trajectory", og, orf)
+    mg, mr = float(np.abs(got - f64).max()), float(np.abs(ref - f64).max())
+    assert mg <= 2 * mr + tol, (name, "largest deviation from the float64 trajectory", mg, mr)
 
 
 def mostly_close(a, b, rtol=1e-3, frac=0.999):
@@ -474,6 +508,7 @@ def test_trainer_step_matches_reference_f7(golden, golden_meta, ref_state):
     meta = golden_meta["F7"]
     tr, _ = _trainer(ref_state)
     t_rand = seeded_uniform(meta["seed_t_rand"], (256, 64), meta["t_rand_sha256"])
+    g64, p64 = f7_float64(ref_state, f7, meta)
     dev = tr.dev
     loss, rgb = tr.forward_backward(torch.from_numpy(f7["o"]).to(dev), torch.from_numpy(f7["d"]).to(dev),
                                     torch.from_numpy(f7["target"]).to(dev), 0, t_rand=t_rand)
@@ -489,8 +524,10 @@ def test_trainer_step_matches_reference_f7(golden, golden_meta, ref_state):
         prm = tr.view(tr.flat, i).detach().cpu()
         if f"idx/{name}" in f7:
             idx = torch.from_numpy(f7[f"idx/{name}"])
-            rel = close_unless_zero_gradient(g.reshape(-1)[idx].numpy(), f7[f"grad/{name}"], 2e-3, name)
-            _params_close(prm.reshape(-1)[idx].numpy(), f7[f"param/{name}"], 1, name, frac=None, rel_g=rel)
+            grads_no_worse_than_reference(g.reshape(-1)[idx].numpy(), f7[f"grad/{name}"],
+                                          g64[name].reshape(-1)[idx], name)
+            params_no_worse_than_reference(prm.reshape(-1)[idx].numpy(), f7[f"param/{name}"],
+                                           p64[name].reshape(-1)[idx], name)
         else:
             assert rel_l2(g.numpy(), f7[f"grad/{name}"]) < 5e-4, name
             ga = np.abs(f7[f"grad/{name}"].astype(np.float64))
@@ -507,7 +544,7 @@ def test_trainer_matches_oracle_over_steps(ref_state):
     opt = None
     focal = cameras.synthetic_focal(800)
     g = torch.Generator().manual_seed(21)
-    rel_g = {}                        # per entry: the smallest |reference gradient| / tensor max over the steps
+    st64, tab64, opt64 = {k: v.double().clone() for k, v in ref_state.items()}, table.double().clone(), None
     for step in range(3):
         c2w = cameras.frame_c2w("chair", "circle", 10 * step, 120).float()
         o_all, d_all = get_rays(800, 800, focal, c2w.to(tr.dev))
@@ -518,24 +555,24 @@ def test_trainer_matches_oracle_over_steps(ref_state):
         img = step % 4
         loss_o, _, grads_o, opt = O.train_step(st, tab, img, o.cpu(), d.cpu(), target, 2.0, 6.0, 64, t_rand,
                                                optimizer=opt)
+        _, _, _, opt64 = O.train_step(st64, tab64, img, o.cpu().double(), d.cpu().double(), target.double(), 2.0, 6.0,
+                                      64, t_rand.double(), optimizer=opt64)
         loss, _ = tr.forward_backward(o, d, target.to(tr.dev), img, t_rand=t_rand)
         assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o), step
         for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
             got = tr.view(tr.grad, i).detach().cpu().numpy()
             assert rel_l2(got, grads_o[n].numpy()) < 5e-4, (step, n, rel_l2(got, grads_o[n].numpy()))
-            ga = np.abs(grads_o[n].double().numpy())
-            r = ga / max(ga.max(), 1e-30)
-            rel_g[n] = r if n not in rel_g else np.minimum(rel_g[n], r)
         tr.optimizer_step()
     torch.cuda.synchronize()
     names = list(O.STATE_KEYS) + ["appearance_embeddings"]
     params = dict(st, appearance_embeddings=tab)
+    params64 = dict(st64, appearance_embeddings=tab64)
     for i, n in enumerate(names):
         got = tr.view(tr.flat, i).detach().cpu().numpy()
         exp = params[n].detach().numpy()
-        # an entry may differ (within the 2*lr*steps bound) only where its reference gradient was ~0
-        # at one of the steps: there Adam's first moves take the sign of the rounding
-        _params_close(got, exp, 3, n, frac=None, rel_g=rel_g[n])
+        # the GPU's three steps stay as close to the float64 trajectory as the oracle's fp32 CPU steps
+        params_no_worse_than_reference(got, exp, params64[n].detach().numpy(), n)
+        assert np.abs(got - exp).max() <= 2 * 5e-4 * 3 + 2e-6, n     # and within the flip bound of it
 
 
 def test_training_reduces_loss_on_teacher_scene():
@@ -631,6 +668,8 @@ def test_no_appearance_model_trains_like_the_oracle(noapp_state):
     t_rand = torch.rand(512, 64, generator=g)
     st = {k: v.clone() for k, v in noapp_state.items()}
     loss_o, _, grads_o, opt = O.train_step(st, None, 0, o.cpu(), d.cpu(), target, 2.0, 6.0, 64, t_rand)
+    st64 = {k: v.double().clone() for k, v in noapp_state.items()}
+    O.train_step(st64, None, 0, o.cpu().double(), d.cpu().double(), target.double(), 2.0, 6.0, 64, t_rand.double())
     loss, _ = tr.forward_backward(o, d, target.to(tr.dev), 0, t_rand=t_rand)
     assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o)
     for i, k in enumerate(O.STATE_KEYS):
@@ -641,6 +680,5 @@ def test_no_appearance_model_trains_like_the_oracle(noapp_state):
     sd = tr.optimizer_state_dict()
     assert len(sd["param_groups"][0]["params"]) == 22 and sorted(sd["state"]) == list(range(22))
     for k in noapp_state:
-        ga = np.abs(grads_o[k].double().numpy())
-        _params_close(model.state_dict()[k].cpu().numpy(), st[k].detach().numpy(), 1, k, frac=None,
-                      rel_g=ga / max(ga.max(), 1e-30))
+        params_no_worse_than_reference(model.state_dict()[k].cpu().numpy(), st[k].detach().numpy(),
+                                       st64[k].detach().numpy(), k)
