@@ -2082,196 +2082,6 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a once
 }
 
-// The 256-column weight gradient with both operands staged by LDS-DMA in whole 128-byte lines
-// (tile-major rows only).  wgrad_bf256w_kernel loads its operands fragment-shaped: one dword per lane,
-// each wave-instruction touching eight 32-byte pieces of eight cache lines, and its timing-only
-// ablations put the loads, not the split or the MFMAs, at the top of its cost (§8).  Here a stage
-// (16 samples: the first or second half of a 32-sample tile) of a and of x is copied by 32
-// `global_load_lds_dwordx4` pieces of 1 KiB (8 per wave): piece j takes feature groups j and j + 16
-// (512 contiguous bytes each) into slot j of the stage's image, slots 1,056 bytes apart.  Element
-// (group g, sample s, feature f % 8) sits at slot g % 16, byte (g / 16) * 512 + 32 s + 4 (f % 8): a
-// lane (c, h) of an MFMA fragment reads its 8 samples of feature 32 i + c with ds_read_b32, and the
-// 32-byte pad makes the four groups of a 32-lane half land on disjoint banks.  Each wave splits the
-// raw fragments it reads (a: all NRT row tiles, x: its own 64 columns) into bf16 x 3 itself: no
-// split pass, no second LDS image.  Four stage images (132 KiB) with DMA three stages ahead; a
-// stage is published by a counted vmcnt of the wave's own pieces and a raw s_barrier (LDS-DMA is a
-// pending write on vmcnt: __syncthreads would drain every stage in flight).  The pieces are inline
-// asm as in the weight streams (M0 set per piece; scripts/check_isa.py checks this kernel too).
-// Same bf16x6 arithmetic and partial layout as wgrad_bf256w_kernel; the bias column: each lane sums
-// its 8 samples of a fragment in fp32 and accumulates those in double (every wave, every row tile,
-// branch-free), the two lane halves added once; wave i % 4 writes tile i.
-// Samples 2p, 2p+1 of split3_bf16 (the LDS-DMA kernel spreads a fragment's split over its MFMAs).
-__device__ __forceinline__ void split3_pair(const float (&v)[8], int p, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-#pragma unroll
-  for (int j = 2 * p; j < 2 * p + 2; ++j) {
-    const __bf16 h0 = (__bf16)v[j];
-    const float r1 = v[j] - (float)h0;
-    const __bf16 h1 = (__bf16)r1;
-    const float r2 = r1 - (float)h1;
-    p0[j] = h0;
-    p1[j] = h1;
-    p2[j] = (__bf16)r2;
-  }
-}
-constexpr int kDmaSlot = 1056;                       // bytes per slot: two 512-byte half-groups + pad
-constexpr int kDmaMat = 16 * kDmaSlot;               // one operand's stage image
-constexpr int kDmaStage = 2 * kDmaMat;               // a then x
-constexpr int kDmaStages = 4;
-
-__device__ __forceinline__ void wg_dma_piece(uint32_t voff, const char* src, uint32_t lds) {
-  asm volatile(
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, %1"
-      :
-      : "v"(voff), "s"(src), "s"(lds)
-      : "memory", "m0");
-}
-
-template <int NRT = 8>
-__global__ void __launch_bounds__(256, 1)
-wgrad_dma256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                    int clen, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) char ring[kDmaStages * kDmaStage];
-  const int chunk = blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wk = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, c = lane & 31;
-  const int nst = (int)((m1 - m0 + 15) / 16);
-  // DMA: this wave's pieces j = 4 wk .. 4 wk + 3; lane l copies 16 bytes of group j + 16 (l / 32)
-  const uint32_t voff = (uint32_t)(4 * wk + 16 * h) * 1024u + (uint32_t)c * 16u;
-  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-  // stage st's image <- stage src's samples (src = st except past the chunk's end, see publish)
-  auto issue = [&](int st, int src) __attribute__((always_inline)) {
-    const int64_t ms = m0 + 16 * (int64_t)src;
-    const char* sa = reinterpret_cast<const char*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8);
-    const char* sx = reinterpret_cast<const char*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8);
-    const uint32_t dst = ring_lds + (uint32_t)(st % kDmaStages) * kDmaStage + (uint32_t)(4 * wk) * kDmaSlot;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wg_dma_piece(voff, sa + i * 1024, dst + i * kDmaSlot);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wg_dma_piece(voff, sx + i * 1024, dst + kDmaMat + i * kDmaSlot);
-  };
-  // fragment reads: lane (c, h), sample 8 h + jj of feature group g: slot g % 16, half g / 16
-  const int lane_off = (c >> 3) * kDmaSlot + h * 256 + (c & 7) * 4;
-  const int x_off = kDmaMat + ((8 * wk) % 16) * kDmaSlot + (wk >> 1) * 512;
-  auto read8 = [&](const char* p, float (&v)[8]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) v[jj] = *reinterpret_cast<const float*>(p + 32 * jj);
-  };
-  auto a_tile = [&](int st, int i) __attribute__((always_inline)) {   // i compile-time after unrolling
-    return ring + (st % kDmaStages) * kDmaStage + lane_off + ((4 * i) % 16) * kDmaSlot + (i / 4) * 512;
-  };
-  auto x_tile = [&](int st, int t) __attribute__((always_inline)) {
-    return ring + (st % kDmaStages) * kDmaStage + lane_off + x_off + 4 * t * kDmaSlot;
-  };
-  f32x16 acc[NRT][2];
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  double bacc[NRT];                  // bias column of every row tile (the wave with i % 4 == wk writes tile i)
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) bacc[i] = 0.0;
-  auto bias_add = [&](int i, const float (&v)[8], float keep) __attribute__((always_inline)) {
-    const float s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-    bacc[i] += (double)(s * keep);
-  };
-  // publish(st): this wave's pieces of stage st landed (younger: exactly those of st+1), barrier,
-  // then stage st+2's pieces into the image of stage st-2.  Stage st+1 is published while stage st
-  // is computed, so the next stage's first a tile and x fragments are read in this stage's shadow.
-  // Branch-free: a stage past the chunk re-reads the chunk's last stage into its (free) image, so the
-  // wait is always vmcnt(8) and every path through the kernel issues and publishes the same pieces
-  // (scripts/check_isa.py proves the counts on the ISA's control-flow graph; a conditional issue
-  // would give it paths the hardware never takes).  The pieces still in flight at the end are
-  // drained before the partial is written.
-  auto publish = [&](int st) __attribute__((always_inline)) {
-    wait_vmcnt<8>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    issue(st + 2, st + 2 < nst ? st + 2 : nst - 1);
-  };
-  issue(0, 0);
-  issue(1, 1 < nst ? 1 : 0);
-  publish(0);
-  float vb[8], vx[2][8];              // raw: the next tile's a fragment, the next stage's x
-  bf16x8 fa[3], fx[2][3], fxn[2][3];  // split: this tile's a, this stage's x, the next stage's x
-  {
-    float va[8];
-    read8(a_tile(0, 0), va);
-    read8(x_tile(0, 0), vx[0]);
-    read8(x_tile(0, 1), vx[1]);
-    read8(a_tile(0, 1), vb);
-    bias_add(0, va, 1.0f);
-    WG_SPLIT(va, fa[0], fa[1], fa[2]);
-    WG_SPLIT(vx[0], fx[0][0], fx[0][1], fx[0][2]);
-    WG_SPLIT(vx[1], fx[1][0], fx[1][1], fx[1][2]);
-  }
-  // stage st, tile step i: the reads of tile i+2 (tiles past NRT-1: the next stage's, published with
-  // this stage), tile i's 12 MFMAs with the split of tile i+1 (read one step earlier) in their shadow.
-  // The next stage's x is read in step 0 and split in steps 1 and 2.
-  for (int st = 0; st < nst; ++st) {
-    publish(st + 1);
-    const int sn = st + 1 < nst ? st + 1 : st;   // past the last stage: harmless reads of this one
-    const float keep = st + 1 < nst ? 1.0f : 0.0f;   // ... that add nothing to the bias
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      float vc[8];
-      read8(i + 2 < NRT ? a_tile(st, i + 2) : a_tile(sn, i + 2 - NRT), vc);
-      if (i == 0) {
-        read8(x_tile(sn, 0), vx[0]);
-        read8(x_tile(sn, 1), vx[1]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // the 12 MFMAs in source order, each followed by one item of VALU work and a scheduling fence:
-      // items 0-3 split tile i+1 (two samples each), 4 its bias, 5-8 (steps 1 and 2) a next-stage x
-      bf16x8 fan[3];
-      f32x16 t0 = acc[i][0], t1 = acc[i][1];
-#pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        const int j = k / 6, q = k % 6;
-        const bf16x8& A = fa[q == 0 || q == 3 || q == 5 ? 0 : (q == 1 || q == 4 ? 1 : 2)];
-        const bf16x8& B = fx[j][q == 0 ? 2 : (q == 1 || q == 3 ? 1 : 0)];
-        if (j == 0) t0 = mfma_bf16(A, B, t0);
-        else t1 = mfma_bf16(A, B, t1);
-        if (k < 4) split3_pair(vb, k, fan[0], fan[1], fan[2]);
-        if (k == 4) bias_add(i + 1 < NRT ? i + 1 : 0, vb, i + 1 < NRT ? 1.0f : keep);
-        if (i == 1 && k >= 5 && k < 9) split3_pair(vx[0], k - 5, fxn[0][0], fxn[0][1], fxn[0][2]);
-        if (i == 2 && k >= 5 && k < 9) split3_pair(vx[1], k - 5, fxn[1][0], fxn[1][1], fxn[1][2]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      acc[i][0] = t0;
-      acc[i][1] = t1;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = fan[p];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) vb[jj] = vc[jj];
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) fx[t][q] = fxn[t][q];
-  }
-  wait_vmcnt<0>();                   // the past-the-end pieces land before the workgroup's LDS is released
-  constexpr int KP = kWT + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(32 * NRT, kWT);
-#pragma unroll
-  for (int i = 0; i < NRT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-    }
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) {
-    const double b = bacc[i] + __shfl_xor(bacc[i], 32);
-    if (i % 4 == wk && h == 0) out[(size_t)(32 * i + c) * KP + kWT] = (float)b;
-  }
-}
-
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2508,11 +2318,6 @@ static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, 
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
 // appearance projection's x (the embedding rows, one per ray) is row-major: x_tiled = false.
-#ifdef NERF_WG_DMA
-constexpr bool kWgDma = true;
-#else
-constexpr bool kWgDma = false;
-#endif
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
                  const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true) {
@@ -2528,14 +2333,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
-    if (kWgDma && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk && clen % 16 == 0) {
-      // LDS-DMA operand staging (tile-major rows): 256 rows, or dir_linear + the density head (160)
-      if (N == 160)
-        hipLaunchKernelGGL(wgrad_dma256_kernel<5>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-      else
-        hipLaunchKernelGGL(wgrad_dma256_kernel<8>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-      rc = check_launch("wgrad_dma256_kernel");
-    } else if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
+    if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
       hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                          ws);
       rc = check_launch("wgrad_bf256w_kernel<5>");

@@ -6,7 +6,7 @@ the same disassembly with an M0 reader inserted (explicit operand, implicit read
 not consume).
 
 vmcnt: every publish of an LDS-DMA ring (the counted `s_waitcnt vmcnt(N)` + `s_barrier` of
-stream16.h, train.hip's bw_publish and wgrad_dma256_kernel) must leave in flight only pieces younger
+stream16.h, train.hip's bw_publish) must leave in flight only pieces younger
 than the published chunk, on every path of the kernel's control-flow graph.  Shown on the shipped
 library (passes), on the shipped disassembly with one publish over-counted, a flat op in the window
 or the exit drain removed (fails), and on committed disassemblies of three builds
@@ -133,8 +133,7 @@ def test_unconsumed_m0_write_is_caught(disasm):
 # ---- counted vmcnt waits of the LDS-DMA streams (check_isa.check_vmcnt) ---------------------------
 def test_stream_kernels_are_checked(disasm):
     report, checked = check_isa.check(disasm)
-    for k in ("mlp16_kernel<true>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel",
-              "wgrad_dma256_kernel<8>", "wgrad_dma256_kernel<5>"):
+    for k in ("mlp16_kernel<true>", "mlp16_kernel<false>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel"):
         assert any(k in n for n in checked), k
     assert report == {}, report
 
@@ -157,7 +156,7 @@ def _publish_waits(text, kernel):
     return lines, out
 
 
-@pytest.mark.parametrize("kernel", ["mlp16_kernel<true>", "mlp_backward16_bound_kernel", "wgrad_dma256_kernel<8>"])
+@pytest.mark.parametrize("kernel", ["mlp16_kernel<true>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel"])
 def test_overcounted_publish_wait_is_caught(disasm, kernel):
     """One publish wait counting one op more than issued after its chunk's pieces, in the ISA text."""
     lines, waits = _publish_waits(disasm, kernel)
