@@ -106,7 +106,7 @@ __device__ __forceinline__ void mask_or(const SaveAt& sv, int T, uint32_t bits) 
 // one store instruction writes the wave's 32 samples x 8 features, 1 KiB, contiguously)
 __device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sv.rows, (int)sv.loff + 4 * (int)tile_col(c),
-                                         4 * (int)tile_col(sv.hoff), 0);
+                                         4 * (int)tile_col(sv.hoff), kRowStoreAux);
 }
 template <int T0, int QG, bool SIGMA>
 __device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {

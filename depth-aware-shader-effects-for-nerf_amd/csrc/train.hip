@@ -1026,7 +1026,8 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
   }
 #ifndef NERF_BW_NO_STORES   // (timing-only A/B build: the cost of the gradient-row stores)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
-                                         (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice), 0);
+                                         (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice),
+                                         kRowStoreAux);
 #endif
   if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
     Operand& op = in[OP0 + QG / 2];
@@ -1612,7 +1613,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
     for (int q = 0; q < SA; ++q)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        ra[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[q][j], 0, 0));
+        ra[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo[q][j], 0, kRowLoadAux));
     if constexpr (XD1) {
       const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
@@ -1621,7 +1622,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
       for (int q = 0; q < SX; ++q)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xs, (int)xvo[q][j], 0, 0));
+          rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xs, (int)xvo[q][j], 0, kRowLoadAux));
       return;
     }
 #pragma unroll
@@ -1633,7 +1634,7 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
       for (int j = 0; j < 8; ++j) {
         const bool ok = rel + j < mrel_end && xcol[q] != kOut;
         const uint32_t off = ok ? row * ldx4 + xcol[q] : kOut;
-        rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)off, 0, 0));
+        rx[SET][q][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)off, 0, kRowLoadAux));
         if (++r == xd) {
           r = 0;
           ++row;
@@ -1851,12 +1852,12 @@ wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __rest
         BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0)));
+      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux)));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0)));
+        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux)));
   };
   auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
@@ -1980,12 +1981,12 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
         BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0)));
+      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux)));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0)));
+        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux)));
   };
   bf16x8 fx[2][2][3];                // split x fragments of stages st (fx[st & 1]) and st+1
   auto split_x = [&](auto set_c, auto fb_c) __attribute__((always_inline)) {
@@ -2124,10 +2125,10 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
         BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0));
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * xs4), 0));
+      rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * xs4), kRowLoadAux));
   };
   auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
