@@ -184,13 +184,6 @@ __device__ __forceinline__ void pe_operand(const float* pe_mine, float s, Operan
 // SAVE = the training forward (nerf_mlp_forward_train): also writes each sample's activation row
 // (layout.h kSave*: h_0..h_7 from the epilogue quarters, enc_x, enc_d, r_dir, hd from the heads)
 // to `save` (M x kSaveRow); encd (R x 32) holds each ray's PE_4(d) from nerf_ray_features.
-//
-// Render (SAVE = false): a persistent block loop.  The grid holds one workgroup per CU and each
-// workgroup runs sample blocks blockIdx.x, + gridDim.x, ... (128 samples each).  Between blocks
-// nothing drains: the small vectors stay in LDS, the colour layer already streams the next block's
-// first three weight chunks (the stream wraps, stream16.h WRAP) and publishes its chunk 0, and the
-// next block's positions are loaded while the colour layer runs.  A block's exposed work is its PE
-// and its heads; the dispatch of a new workgroup, its LDS fill and the stream's first chunks went.
 template <bool SAVE>
 __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
@@ -198,411 +191,333 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
              float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
              float* __restrict__ save, const float* __restrict__ encd, uint32_t* __restrict__ masks) {
   __shared__ __attribute__((aligned(16))) float lds[SAVE ? kLdsFloatsSave : kLdsFloats];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane0 = threadIdx.x & 63, h0 = lane0 >> 5;
-  const int64_t nblk = (M + 32 * kW16Waves - 1) / (32 * kW16Waves);
-  const int64_t bstride = SAVE ? nblk : (int64_t)gridDim.x;   // SAVE: one block per workgroup
-  int64_t blk = blockIdx.x;
-  int64_t s0 = (blk * kW16Waves + wave) * 32;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
   STAMP16(0);
-  // Sample positions of block bk for this lane: pts = o + d*z with separate roundings
-  // (ray_utils.py:86), or the points themselves (zv == nullptr); and the output slot.
-  struct Pos {
-    float a[3], b[3], z;
-    int slot;
-  };
-  auto fetch = [&](int64_t bk, Pos& p) __attribute__((always_inline)) {
-    const int64_t b0 = (bk * kW16Waves + wave) * 32;
-    const int64_t ss = imin64(b0 + (lane0 & 31), M - 1);
-    if (zv) {
-      const int64_t rr = ss / N;
-      p.z = zv[ss];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        p.a[c] = orig[3 * rr + c];
-        p.b[c] = dirs[3 * rr + c];
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) p.a[c] = orig[3 * ss + c];
-    }
-    p.slot = out_slot && b0 + (lane0 & 31) < M ? out_slot[ss] : 0;
-  };
-  Pos cur;
-  fetch(blk, cur);
+  const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
+  // every wave runs to the end (the weight stream has barriers); tail lanes repeat sample M-1
+  const bool valid = s0 + (lane & 31) < M;
+  const int64_t s = imin64(s0 + (lane & 31), M - 1);
+  const int64_t r = s / N;
   // training: the wave's activation rows (uniform) and this lane's offset into them
   __amdgpu_buffer_rsrc_t wrows;
   if constexpr (SAVE)
     wrows = __builtin_amdgcn_make_buffer_rsrc(save + s0 * kSaveRow, (short)0, 32 * kSaveRow * 4, 0x00020000);
+  // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
+  // inside the MFMA schedule)
+  const uint32_t loff = valid ? ((uint32_t)(lane & 31) * 8 + 4 * h) * 4 : 0x40000000u;
   // training: this wave's mask rows in LDS, zeroed before the quarters OR their bits in
   unsigned* mwave = reinterpret_cast<unsigned*>(lds + kLdsMask) + wave * 32 * kMaskWords;
+  unsigned* mrow = mwave + (lane & 31) * kMaskWords + 4 * h;
   if constexpr (SAVE) {
-    for (int i = lane0; i < 32 * kMaskWords; i += 64) mwave[i] = 0u;
+    for (int i = lane; i < 32 * kMaskWords; i += 64) mwave[i] = 0u;
   }
-  // Small vectors into LDS (once per workgroup), then the weight stream starts: chunks 0-2 in flight
-  // while the PE is computed (every ordinary load retired first, see the LDS note).
+
+  // Sample position: pts = o + d*z with separate roundings (ray_utils.py:86).
+  float x[3];
+  if (zv) {
+    const float z = zv[s];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) x[c] = orig[3 * r + c] + dirs[3 * r + c] * z;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) x[c] = orig[3 * s + c];
+  }
+  // Small vectors into LDS, then the weight stream starts: chunks 0-2 in flight while the PE is
+  // computed (every ordinary load retired first, see the LDS note).
   for (int i = threadIdx.x; i < kLdsVecFloats / 4; i += 64 * kW16Waves)
     reinterpret_cast<f32x4*>(lds + kLdsBias)[i] = reinterpret_cast<const f32x4*>(packed + kOffBias)[i];
   if (threadIdx.x < kS16Consts) lds[kLdsConsts + threadIdx.x] = packed[kOffScale16 + threadIdx.x];
   if (threadIdx.x < kLdsRgbFloats / 4)
     reinterpret_cast<f32x4*>(lds + kLdsRgb)[threadIdx.x] = reinterpret_cast<const f32x4*>(packed + kOffRgbW)[threadIdx.x];
+  const int slot = out_slot && valid ? out_slot[s] : 0;
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_sched_barrier(0);
-  const float* stream0 = packed + kOff16;
+  const float* stream = packed + kOff16;
   const uint32_t lds_dma = (uint32_t)(uintptr_t)(lptr_t)lds + 1024u * wave;   // this wave's first piece
-  const uint32_t voff = 16u * lane0 + 1024u * wave;
-  chunk_dma<0>(stream0, 0, lds_dma, voff);
-  chunk_dma<1>(stream0, 1, lds_dma, voff);
-  chunk_dma<2>(stream0, 2, lds_dma, voff);
-  h16x8 a0[4][2], a1[4][2];
-  if constexpr (!SAVE) {
-    // publish chunk 0 before the first block's PE (every block then starts as the previous block's
-    // colour layer leaves the stream: chunk 0 published, a0 = its k-step 0, chunks 1-2 in flight;
-    // one stream structure on every path, which scripts/check_isa.py verifies)
-    wait_vmcnt<8>();
-    __builtin_amdgcn_s_barrier();
-    read_kstep<0>(lds, a0, lane0);
+  const uint32_t voff = 16u * lane + 1024u * wave;
+  chunk_dma<0>(stream, 0, lds_dma, voff);
+  chunk_dma<1>(stream, 1, lds_dma, voff);
+  chunk_dma<2>(stream, 2, lds_dma, voff);
+
+  // PE in layout.h::pe_feature order (models.py:36-44): sin on lane half 0, cos on half 1.
+  // pe_sin.h: one reduction + both polynomials per value; a wave with a coordinate beyond its
+  // range (|x| 2^9 > kPeSinMax) takes the library sincosf.
+  float pe[kPeSteps];
+  const float ax = fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2])));
+  if (__any(ax * (float)(1 << (kPosLevels - 1)) > kPeSinMax)) {
+#pragma unroll
+    for (int i = 0; i < kPosLevels; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float sn, cs;
+        sincosf(x[c] * (float)(1 << i), &sn, &cs);
+        pe[3 * i + c] = h ? cs : sn;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kPosLevels; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pe[3 * i + c] = pe_sin_reduced(x[c] * (float)(1 << i), h);
   }
+  pe[30] = h ? x[1] : x[0];
+  pe[31] = h ? 0.0f : x[2];
+  float* pe_mine = lds + kLdsPe + wave * kPeSteps * 64;
+#pragma unroll
+  for (int p = 0; p < kPeSteps; ++p) pe_mine[p * 64 + lane] = pe[p];
+  const float m_pe = fmaxf(1.0f, fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2]))));   // bounds |PE|
+
   const float* bias = lds + kLdsBias;
   const float* ws = lds + kLdsSigmaW;
   const float* cst = lds + kLdsConsts;
-  float* pe_mine = lds + kLdsPe + wave * kPeSteps * 64;
-  float* feat_mine = lds + kLdsFeat + wave * kRayFeat;
-  const float* wr = lds + kLdsRgb;
-  // when N is a multiple of 32 the wave's 32 samples lie on one ray (see the colour layer)
-  const bool one_ray = (N & 31) == 0;
+  // s_cur: scale of the current layer's inputs; inv_cur unscales its accumulators; s_nxt: scale
+  // of the next layer's inputs (from the bound on this layer's outputs).
+  float s_cur = pow2_scale(m_pe);
+  Operand pe_op[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split_into(pe[8 * q + j] * s_cur, pe_op[q], j);
+
+  wait_vmcnt<8>();                                          // this wave's part of chunk 0 (chunks 1-2 in flight)
+  __builtin_amdgcn_s_barrier();
+  h16x8 a0[4][2], a1[4][2];
+  read_kstep<0>(lds, a0, lane);
+
   f32x16 acc[8];
   Operand in[16];
+  float m = 0.0f, part = 0.0f;
+  float inv_cur = cst[kS16InvW + 0] / s_cur;                // exact: powers of two
+  float s_nxt = pow2_scale(cst[kS16R + 0] * m_pe + cst[kS16B + 0]);
+  STAMP16(1);
+
+  // ---- layer 0: PE(63) -> 256, 2 chunk-steps per group ----
+  auto pe_operand_of = [&](auto i, auto kk) -> const Operand& { return pe_op[kstep_of(i, kk)]; };
+  run_group<0, 2, 0, 3, kSideNone, SAVE>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
+  // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE),
+  // 4 quarters per half-step
   QuarterVec qv[4];
   float pe_v[8];
-#pragma unroll 1
-  for (;;) {
-    // the stream's base, opaque to the compiler per block: otherwise it hoists every chunk's piece
-    // addresses (loop-invariant) out of the block loop and spills the SGPRs that hold them
-    const float* stream = stream0;
-    asm volatile("" : "+s"(stream));
-    // (likewise the lane: every per-lane LDS address derives from it, and hoisted out of the loop
-    // they spill)
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
-    const int h = lane >> 5;
-    unsigned* mrow = mwave + (lane & 31) * kMaskWords + 4 * h;
-    s0 = (blk * kW16Waves + wave) * 32;
-    // every wave runs to the end (the weight stream has barriers); tail lanes repeat sample M-1
-    const bool valid = s0 + (lane & 31) < M;
-    const int64_t s = imin64(s0 + (lane & 31), M - 1);
-    const int64_t r = s / N;
-    const bool has_next = !SAVE && blk + bstride < nblk;       // uniform over the workgroup
-    // a tail lane's offset lies past the rows' buffer range, so its stores are dropped (no branch
-    // inside the MFMA schedule)
-    const uint32_t loff = valid ? ((uint32_t)(lane & 31) * 8 + 4 * h) * 4 : 0x40000000u;
-    float x[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) x[c] = zv ? cur.a[c] + cur.b[c] * cur.z : cur.a[c];
-    const int slot = cur.slot;
+  SaveAt sv_prev{wrows, loff, save_h(0), valid, mrow, 0};   // training: save slices of y_{L-1}, y_L
+  SaveAt sv_cur = sv_prev;
+  run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
+                                       [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                         constexpr int hs = kstep_of(i, kk);
+                                         static_for<4>([&](auto qc) __attribute__((always_inline)) {
+                                           constexpr int j = decltype(qc)::value;
+                                           quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false, SAVE>(
+                                               acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j], sv_cur);
+                                         });
+                                       });
+  STAMP16(2);
 
-    // PE in layout.h::pe_feature order (models.py:36-44): sin on lane half 0, cos on half 1.
-    // pe_sin.h: one reduction + both polynomials per value; a wave with a coordinate beyond its
-    // range (|x| 2^9 > kPeSinMax) takes the library sincosf.
-    float pe[kPeSteps];
-    const float ax = fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2])));
-    if (__any(ax * (float)(1 << (kPosLevels - 1)) > kPeSinMax)) {
+  // ---- layers 1..7 ----
+  // On entry to layer L: operands 0..7 hold y_{L-1} tiles 0-3 split at s_cur, y_{L-1} tiles 4-7
+  // wait in acc[4..7], m holds the max of ReLU(y_{L-1}) tiles 0-3.
+  //
+  // Side-work schedule, by half-step hs of a group (one k-step), in quarter tiles (4 registers of a
+  // tile, ~40 VALU instructions, spread over the half-step's 12 MFMA gaps):
+  //  * group A converts y_{L-1} tiles 4-7 into operands 8..15: quarters 0, 1 at hs 0, quarter
+  //    hs + 1 at hs 1..14.  Operand 8+j (quarters 2j, 2j+1) is complete at hs 2j and first read at
+  //    hs 8+j; acc[4..7] is free again before group B;
+  //  * group B converts this layer's y_L tiles 0-3 into operands 0..7: quarter hs - 1 at hs 1..14,
+  //    quarters 14, 15 at hs 15.  Operand j was last read at hs j, and is next read at the next
+  //    layer's hs j.
+  float inv_prev = inv_cur;
+  const float* bias_prev = bias;
+  s_cur = s_nxt;
+  auto act_operand = [&](auto i, auto kk) -> const Operand& { return in[kstep_of(i, kk)]; };
+  auto op4 = [&](auto i, auto kk) -> const Operand& {
+    constexpr int ks = kstep_of(i, kk);
+    if constexpr (ks < 16) return in[ks];
+    else return pe_op[ks - 16];
+  };
+  // group A's side: y_{L-1} tiles 4-7 (SIGMA: also the density head's dot product)
+  auto side_prev = [&](auto i, auto kk, auto ph, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
+    constexpr bool sg = decltype(sigma_tag)::value;
+    if constexpr (hs == 0) {
+      quarter<P, 4, 8, 0, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
+      quarter<P, 4, 8, 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1], sv_prev);
+    } else if constexpr (hs <= 14) {
+      quarter<P, 4, 8, hs + 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
+    }
+  };
+  // group B's side: this layer's y_L tiles 0-3
+  auto side_cur = [&](auto i, auto kk, auto ph, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
+    constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
+    constexpr bool sg = decltype(sigma_tag)::value;
+    if constexpr (hs >= 1 && hs <= 14) {
+      quarter<P, 0, 0, hs - 1, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
+    } else if constexpr (hs == 15) {
+      quarter<P, 0, 0, 14, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
+      quarter<P, 0, 0, 15, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1], sv_cur);
+    }
+  };
+  using NoSigma = std::false_type;
+  using Sigma = std::true_type;
+#pragma unroll 1
+  for (int L = 1; L < 8; ++L) {
+    inv_cur = cst[kS16InvW + L] / s_cur;
+    const float* bias_l = bias + L * kHidden;
+    const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
+    if constexpr (SAVE) {
+      sv_prev.hoff = save_h(L - 1);
+      sv_cur.hoff = save_h(L);
+      sv_prev.mlay = (kMaskLayerBytes / 4) * (L - 1);
+      sv_cur.mlay = (kMaskLayerBytes / 4) * L;
+    }
+    // group A (k-steps 0..15, + PE 16..19 at layer 4)
+    if (L == kSkipLayer) {
+      // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
+      // read at hs 16 + q)
+      run_group<0, 10, 0, 3, kSideSkipPrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+                                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
+                                              constexpr int hs = kstep_of(i, kk);
+                                              side_prev(i, kk, ph, NoSigma{});
+                                              if constexpr (hs >= 15 && hs < 19)
+                                                pe_operand<decltype(ph)::value, hs - 15>(pe_mine, s_cur, pe_op[hs - 15],
+                                                                                         pe_v, lane);
+                                            });
+    } else {
+      run_group<0, 8, 0, 3, kSidePrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, NoSigma{}); });
+    }
+    // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
+    m = sample_max(m);
+    float bound = cst[kS16R + L] * (L == kSkipLayer ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
+    if (L + 1 == kSkipLayer) bound = fmaxf(bound, m_pe);    // layer 4 splits the PE at the same scale
+    s_nxt = pow2_scale(bound);
+    m = 0.0f;
+    // group B (layer 7 also starts the density head)
+    if (L == kSkipLayer) {
+      run_group<1, 10, 2, 3, kSideCur, SAVE>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
+                             [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
+    } else if (L == 7) {
+      run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, Sigma{}); });
+    } else {
+      run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
+    }
+    inv_prev = inv_cur;
+    bias_prev = bias_l;
+    s_cur = s_nxt;
+    STAMP16(2 + L);
+  }
+
+  // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
+  // operands 8..15 and finishes the density head ----
+  // When N is a multiple of 32 the wave's 32 samples lie on one ray: its 1 KiB of ray features
+  // (b_dir + W_dd PE(d) | appearance) is DMA'd into this wave's LDS area while the colour layer
+  // runs (the stream's last vmcnt(0) covers it), so the heads read LDS, not HBM.
+  const bool one_ray = (N & 31) == 0;
+  float* feat_mine = lds + kLdsFeat + wave * kRayFeat;
+  if (one_ray) {
+    const char* src = reinterpret_cast<const char*>(feat + (imin64(s0, M - 1) / N) * kRayFeat);   // tail waves: last ray
+    const uint32_t dst = (uint32_t)(uintptr_t)(lptr_t)feat_mine;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(16u * lane), "s"(src), "s"(dst)
+        : "memory");
+  }
+  inv_cur = cst[kS16InvW + 8] / s_cur;
+  if constexpr (SAVE) {
+    sv_prev.hoff = save_h(7);
+    sv_prev.mlay = (kMaskLayerBytes / 4) * 7;
+  }
+  run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
+                        [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
+  STAMP16(10);
+
+  // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
+  const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
+  // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
+  // (models.py:141-156); the bracket and the appearance part come per ray in `feat`.
+  const float* wr = lds + kLdsRgb;
+  float pr[3] = {0.0f, 0.0f, 0.0f};
+  auto colour_head = [&](const float* fr) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < kPosLevels; ++i)
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 fd = *reinterpret_cast<const f32x4*>(fr + t * 32 + 8 * q + 4 * h);
+        const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
+        f32x4 rd, hd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f);
+          hd[e] = rd[e] + ap[e];
+        }
+        if constexpr (SAVE) {
+          const SaveAt at{wrows, loff, 0, true, mrow, 0};
+          save_store(at, kSaveRDir + t * 32 + 8 * q, rd);
+          save_store(at, kSaveHd + t * 32 + 8 * q, hd);
+          uint32_t bits = 0u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bits |= (rd[e] > 0.0f ? 1u : 0u) << (16 * (t % 2) + 4 * q + e);
+          // r_dir: 8 bytes per lane half at byte 256 + 8h of the row (mrow holds + 4h words)
+          __hip_atomic_fetch_or(mrow - 2 * h + kMaskRDirByte / 4 + t / 2, bits, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          float sn, cs;
-          sincosf(x[c] * (float)(1 << i), &sn, &cs);
-          pe[3 * i + c] = h ? cs : sn;
-        }
-    } else {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
 #pragma unroll
-      for (int i = 0; i < kPosLevels; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) pe[3 * i + c] = pe_sin_reduced(x[c] * (float)(1 << i), h);
-    }
-    pe[30] = h ? x[1] : x[0];
-    pe[31] = h ? 0.0f : x[2];
-#pragma unroll
-    for (int p = 0; p < kPeSteps; ++p) pe_mine[p * 64 + lane] = pe[p];
-    const float m_pe = fmaxf(1.0f, fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2]))));   // bounds |PE|
-
-    // s_cur: scale of the current layer's inputs; inv_cur unscales its accumulators; s_nxt: scale
-    // of the next layer's inputs (from the bound on this layer's outputs).
-    float s_cur = pow2_scale(m_pe);
-    Operand pe_op[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) split_into(pe[8 * q + j] * s_cur, pe_op[q], j);
-
-    if constexpr (SAVE) {
-      wait_vmcnt<8>();                                      // this wave's part of chunk 0 (chunks 1-2 in flight)
-      __builtin_amdgcn_s_barrier();
-      read_kstep<0>(lds, a0, lane);
-    }
-    float m = 0.0f, part = 0.0f;
-    float inv_cur = cst[kS16InvW + 0] / s_cur;                // exact: powers of two
-    float s_nxt = pow2_scale(cst[kS16R + 0] * m_pe + cst[kS16B + 0]);
-    STAMP16(1);
-
-    // ---- layer 0: PE(63) -> 256, 2 chunk-steps per group ----
-    auto pe_operand_of = [&](auto i, auto kk) -> const Operand& { return pe_op[kstep_of(i, kk)]; };
-    run_group<0, 2, 0, 3, kSideNone, SAVE>(stream, 0, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of, NoSide{});
-    // group B converts group A's outputs (tiles 0-3) into operands 0..7 (free: layer 0 reads the PE),
-    // 4 quarters per half-step
-    SaveAt sv_prev{wrows, loff, save_h(0), valid, mrow, 0};   // training: save slices of y_{L-1}, y_L
-    SaveAt sv_cur = sv_prev;
-    run_group<1, 2, 2, 3, kSideL0, SAVE>(stream, 2, lds, lds_dma, voff, a0, a1, acc, lane, pe_operand_of,
-                                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
-                                           constexpr int hs = kstep_of(i, kk);
-                                           static_for<4>([&](auto qc) __attribute__((always_inline)) {
-                                             constexpr int j = decltype(qc)::value;
-                                             quarter<decltype(ph)::value, 0, 0, 4 * hs + j, false, SAVE>(
-                                                 acc, inv_cur, bias, ws, h, s_nxt, in, m, part, qv[j], sv_cur);
-                                           });
-                                         });
-    STAMP16(2);
-
-    // ---- layers 1..7 ----
-    // On entry to layer L: operands 0..7 hold y_{L-1} tiles 0-3 split at s_cur, y_{L-1} tiles 4-7
-    // wait in acc[4..7], m holds the max of ReLU(y_{L-1}) tiles 0-3.
-    //
-    // Side-work schedule, by half-step hs of a group (one k-step), in quarter tiles (4 registers of a
-    // tile, ~40 VALU instructions, spread over the half-step's 12 MFMA gaps):
-    //  * group A converts y_{L-1} tiles 4-7 into operands 8..15: quarters 0, 1 at hs 0, quarter
-    //    hs + 1 at hs 1..14.  Operand 8+j (quarters 2j, 2j+1) is complete at hs 2j and first read at
-    //    hs 8+j; acc[4..7] is free again before group B;
-    //  * group B converts this layer's y_L tiles 0-3 into operands 0..7: quarter hs - 1 at hs 1..14,
-    //    quarters 14, 15 at hs 15.  Operand j was last read at hs j, and is next read at the next
-    //    layer's hs j.
-    float inv_prev = inv_cur;
-    const float* bias_prev = bias;
-    s_cur = s_nxt;
-    auto act_operand = [&](auto i, auto kk) -> const Operand& { return in[kstep_of(i, kk)]; };
-    auto op4 = [&](auto i, auto kk) -> const Operand& {
-      constexpr int ks = kstep_of(i, kk);
-      if constexpr (ks < 16) return in[ks];
-      else return pe_op[ks - 16];
-    };
-    // group A's side: y_{L-1} tiles 4-7 (SIGMA: also the density head's dot product)
-    auto side_prev = [&](auto i, auto kk, auto ph, auto sigma_tag) __attribute__((always_inline)) {
-      constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
-      constexpr bool sg = decltype(sigma_tag)::value;
-      if constexpr (hs == 0) {
-        quarter<P, 4, 8, 0, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
-        quarter<P, 4, 8, 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[1], sv_prev);
-      } else if constexpr (hs <= 14) {
-        quarter<P, 4, 8, hs + 1, sg, SAVE>(acc, inv_prev, bias_prev, ws, h, s_cur, in, m, part, qv[0], sv_prev);
-      }
-    };
-    // group B's side: this layer's y_L tiles 0-3
-    auto side_cur = [&](auto i, auto kk, auto ph, const float* bias_l, auto sigma_tag) __attribute__((always_inline)) {
-      constexpr int hs = kstep_of(i, kk), P = decltype(ph)::value;
-      constexpr bool sg = decltype(sigma_tag)::value;
-      if constexpr (hs >= 1 && hs <= 14) {
-        quarter<P, 0, 0, hs - 1, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
-      } else if constexpr (hs == 15) {
-        quarter<P, 0, 0, 14, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[0], sv_cur);
-        quarter<P, 0, 0, 15, sg, SAVE>(acc, inv_cur, bias_l, ws, h, s_nxt, in, m, part, qv[1], sv_cur);
-      }
-    };
-    using NoSigma = std::false_type;
-    using Sigma = std::true_type;
-#pragma unroll 1
-    for (int L = 1; L < 8; ++L) {
-      inv_cur = cst[kS16InvW + L] / s_cur;
-      const float* bias_l = bias + L * kHidden;
-      const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
-      if constexpr (SAVE) {
-        sv_prev.hoff = save_h(L - 1);
-        sv_cur.hoff = save_h(L);
-        sv_prev.mlay = (kMaskLayerBytes / 4) * (L - 1);
-        sv_cur.mlay = (kMaskLayerBytes / 4) * L;
-      }
-      // group A (k-steps 0..15, + PE 16..19 at layer 4)
-      if (L == kSkipLayer) {
-        // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
-        // read at hs 16 + q)
-        run_group<0, 10, 0, 3, kSideSkipPrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
-                                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) {
-                                                constexpr int hs = kstep_of(i, kk);
-                                                side_prev(i, kk, ph, NoSigma{});
-                                                if constexpr (hs >= 15 && hs < 19)
-                                                  pe_operand<decltype(ph)::value, hs - 15>(pe_mine, s_cur, pe_op[hs - 15],
-                                                                                           pe_v, lane);
-                                              });
-      } else {
-        run_group<0, 8, 0, 3, kSidePrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, NoSigma{}); });
-      }
-      // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
-      m = sample_max(m);
-      float bound = cst[kS16R + L] * (L == kSkipLayer ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
-      if (L + 1 == kSkipLayer) bound = fmaxf(bound, m_pe);    // layer 4 splits the PE at the same scale
-      s_nxt = pow2_scale(bound);
-      m = 0.0f;
-      // group B (layer 7 also starts the density head)
-      if (L == kSkipLayer) {
-        run_group<1, 10, 2, 3, kSideCur, SAVE>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
-                               [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
-      } else if (L == 7) {
-        run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, Sigma{}); });
-      } else {
-        run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
-      }
-      inv_prev = inv_cur;
-      bias_prev = bias_l;
-      s_cur = s_nxt;
-      STAMP16(2 + L);
-    }
-
-    // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
-    // operands 8..15 and finishes the density head ----
-    // When N is a multiple of 32 the wave's 32 samples lie on one ray: its 1 KiB of ray features
-    // (b_dir + W_dd PE(d) | appearance) is DMA'd into this wave's LDS area while the colour layer
-    // runs, so the heads read LDS, not HBM.
-    if (one_ray) {
-      const char* src = reinterpret_cast<const char*>(feat + (imin64(s0, M - 1) / N) * kRayFeat);   // tail waves: last ray
-      const uint32_t dst = (uint32_t)(uintptr_t)(lptr_t)feat_mine;
-      uint32_t keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\t"
-          "s_mov_b32 m0, %3\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %1, %2\n\t"
-          "s_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(16u * lane), "s"(src), "s"(dst)
-          : "memory");
-    }
-    inv_cur = cst[kS16InvW + 8] / s_cur;
-    if constexpr (SAVE) {
-      sv_prev.hoff = save_h(7);
-      sv_prev.mlay = (kMaskLayerBytes / 4) * 7;
-    }
-    auto colour_side = [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); };
-    if constexpr (SAVE) {
-      run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                                             colour_side);
-    } else {
-      // streams and publishes the next block's chunk 0 (a0 = its k-step 0), chunks 1-2 in flight; after
-      // the last block those are drained below, unused
-      run_group<0, 8, 0, 3, kSidePrev, SAVE, true>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane,
-                                                   act_operand, colour_side);
-    }
-    STAMP16(10);
-    // The next block's positions load now, while the heads run (ordinary loads: the compiler waits
-    // for them at their first use, the next block's PE).
-    Pos nxt;
-    if (has_next) fetch(blk + bstride, nxt);
-
-    // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
-    const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
-    // colour branch: h_dir = ReLU(W_dh ReLU(h7) + [b_dir + W_dd PE(d)]) + appearance
-    // (models.py:141-156); the bracket and the appearance part come per ray in `feat`.
-    float pr[3] = {0.0f, 0.0f, 0.0f};
-    auto colour_head = [&](const float* fr) __attribute__((always_inline)) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 fd = *reinterpret_cast<const f32x4*>(fr + t * 32 + 8 * q + 4 * h);
-          const f32x4 ap = *reinterpret_cast<const f32x4*>(fr + kDirHidden + t * 32 + 8 * q + 4 * h);
-          f32x4 rd, hd;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            rd[e] = fmaxf(fmaf(acc[t][4 * q + e], inv_cur, fd[e]), 0.0f);
-            hd[e] = rd[e] + ap[e];
-          }
-          if constexpr (SAVE) {
-            const SaveAt at{wrows, loff, 0, true, mrow, 0};
-            save_store(at, kSaveRDir + t * 32 + 8 * q, rd);
-            save_store(at, kSaveHd + t * 32 + 8 * q, hd);
-            uint32_t bits = 0u;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) bits |= (rd[e] > 0.0f ? 1u : 0u) << (16 * (t % 2) + 4 * q + e);
-            // r_dir: 8 bytes per lane half at byte 256 + 8h of the row (mrow holds + 4h words)
-            __hip_atomic_fetch_or(mrow - 2 * h + kMaskRDirByte / 4 + t / 2, bits, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
-          }
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const f32x4 w = *reinterpret_cast<const f32x4*>(wr + c * kDirHidden + t * 32 + 8 * q + 4 * h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], hd[e], pr[c]);
-          }
-        }
-    };
-    if (one_ray) {
-      // render: the feature piece is older than every piece of the colour layer's stream, so the
-      // stream's last publish wait (for the next block's chunk 0) already covered it; a wait here
-      // would also wait for the next block's chunks 1-2 and the position loads issued after them
-      if constexpr (SAVE) wait_vmcnt<0>();
-      colour_head(feat_mine);
-    } else {
-      colour_head(feat + r * kRayFeat);
-    }
-    if constexpr (SAVE) {   // the wave's 32 mask rows: 8,704 contiguous bytes in LDS and in `masks`
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const int n16 = (int)imin64(M - s0, 32) * (kMaskWords / 4);
-      u32x4v* dst = reinterpret_cast<u32x4v*>(masks + s0 * kMaskWords);
-      for (int i = lane; i < n16; i += 64) dst[i] = reinterpret_cast<const u32x4v*>(mwave)[i];
-    }
-    float out[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
-      out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
-    }
-    if constexpr (SAVE) {
-      if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d
-#pragma unroll
-        for (int p = 0; p < kPeSteps; ++p) {
-          const int f = pe_feature(p, h);
-          const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? 0.0f : pe_mine[p * 64 + lane]), wrows,
-                                                (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
-        }
-        const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
-          const int F = kSaveEncD + 16 * h + 4 * q;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
-                                                 (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+          for (int e = 0; e < 4; ++e) pr[c] = fmaf(w[e], hd[e], pr[c]);
         }
       }
-    }
-    if (h == 0 && valid) {
-      const int64_t o_s = out_slot ? r * out_T + slot : s;
-      sigma[o_s] = sig;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
-    }
-    STAMP16(11);
-    if (!has_next) {
-      if constexpr (!SAVE) wait_vmcnt<0>();   // the unused chunks 0-2 land before the workgroup's LDS is released
-      break;
-    }
-    blk += bstride;
-    cur = nxt;
+  };
+  if (one_ray) {
+    wait_vmcnt<0>();
+    colour_head(feat_mine);
+  } else {
+    colour_head(feat + r * kRayFeat);
   }
-}
-
-// Workgroups of the render kernel's persistent grid: one per CU (the kernel holds one wave per SIMD).
-static int persistent_workgroups() {
-  static int n[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (n[dev] == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    n[dev] = cus;
+  if constexpr (SAVE) {   // the wave's 32 mask rows: 8,704 contiguous bytes in LDS and in `masks`
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int n16 = (int)imin64(M - s0, 32) * (kMaskWords / 4);
+    u32x4v* dst = reinterpret_cast<u32x4v*>(masks + s0 * kMaskWords);
+    for (int i = lane; i < n16; i += 64) dst[i] = reinterpret_cast<const u32x4v*>(mwave)[i];
   }
-  return n[dev];
+  float out[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v = pr[c] + __shfl_xor(pr[c], 32) + wr[3 * kDirHidden + c];
+    out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
+  }
+  if constexpr (SAVE) {
+    if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d
+#pragma unroll
+      for (int p = 0; p < kPeSteps; ++p) {
+        const int f = pe_feature(p, h);
+        const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? 0.0f : pe_mine[p * 64 + lane]), wrows,
+                                              (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+      }
+      const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+      {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
+        const int F = kSaveEncD + 16 * h + 4 * q;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
+                                               (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+      }
+    }
+  }
+  if (h == 0 && valid) {
+    const int64_t o_s = out_slot ? r * out_T + slot : s;
+    sigma[o_s] = sig;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[3 * o_s + c] = out[c];
+  }
+  STAMP16(11);
 }
 
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
@@ -619,10 +534,9 @@ int launch_mlp16(const float* packed, const float* o, const float* d, const floa
   if (save)
     hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
                        feat, rgb, sigma, out_slot, out_T, save, encd, masks);
-  else   // the render kernel loops over sample blocks: at most one workgroup per CU
-    hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)std::min<int64_t>(blocks, persistent_workgroups())),
-                       dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N, feat, rgb, sigma, out_slot, out_T, nullptr,
-                       nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
+                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr, nullptr);
   return check_launch("mlp16_kernel");
 }
 

@@ -188,10 +188,7 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
 //   the slot chunk c-1 used | MFMA k-step 1, reading chunk c+1's k-step-0 A
 // On entry chunk c is published, c+1 and c+2 are in flight and a0 holds k-step 0's fragments.
 // TAIL = chunks left after c, capped at 3: the stream's last steps stop loading and waiting.
-// WRAP (the render kernel's persistent block loop, mlp16.hip): the stream restarts at chunk 0 for the
-// next sample block, so the DMA three chunks ahead wraps modulo the 128-chunk weight stream (a multiple
-// of the 4-slot ring, so every chunk keeps its slot).
-template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, bool SV, bool WRAP, typename Side0, typename Side1>
+template <int G, int SLOT, bool FIRST, int TAIL, int KIND, int HS0, bool SV, typename Side0, typename Side1>
 __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int c, float* lds, uint32_t lds_dma,
                                            uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], const Operand& b0,
                                            const Operand& b1, f32x16 (&acc)[8], int lane, Side0&& side0,
@@ -238,9 +235,7 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
   // MFMA region (after the fragment reads, which the asm's memory clobber keeps ahead of it) the
   // pieces cost 1.2K cycles per layer; issued as a block between the half-steps, 2.4K
   auto dma = [&](auto ti) __attribute__((always_inline)) {
-    if constexpr (TAIL >= 3)
-      chunk_dma_piece<(SLOT + 3) & 3, decltype(ti)::value>(stream, WRAP ? (c + 3) & (kS16Chunks - 1) : c + 3, lds_dma,
-                                                           voff);
+    if constexpr (TAIL >= 3) chunk_dma_piece<(SLOT + 3) & 3, decltype(ti)::value>(stream, c + 3, lds_dma, voff);
   };
   half_step<G, false, (TAIL >= 1), 0, side_vpg<KIND>(HS0 + 1)>(a1, b1, acc, lds + ((SLOT + 1) & 3) * kChunkFloats, a0,
                                                             lane, side1, dma);
@@ -250,14 +245,14 @@ __device__ __forceinline__ void chunk_step(const float* __restrict__ stream, int
 // the B operand of k-step 2i+kk; side(i, kk, phase) is the VALU work placed in that half-step:
 // phase 0 issues its LDS reads, phase 1 computes.
 // TAIL_END = chunks after this group (capped at 3); SV = the side work stores (training forward).
-template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, bool SV, bool WRAP = false, typename Opnd, typename Side>
+template <int G, int NSTEP, int SLOT0, int TAIL_END, int KIND, bool SV, typename Opnd, typename Side>
 __device__ __forceinline__ void run_group(const float* __restrict__ stream, int c0, float* lds, uint32_t lds_dma,
                                           uint32_t voff, h16x8 (&a0)[4][2], h16x8 (&a1)[4][2], f32x16 (&acc)[8],
                                           int lane, Opnd&& operand, Side&& side) {
   static_for<NSTEP>([&](auto ic) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
     constexpr int left = NSTEP - 1 - i + TAIL_END;
-    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i, SV, WRAP>(
+    chunk_step<G, (SLOT0 + i) & 3, i == 0, (left < 3 ? left : 3), KIND, 2 * i, SV>(
         stream, c0 + i, lds, lds_dma, voff, a0, a1, operand(ic, std::integral_constant<int, 0>{}),
         operand(ic, std::integral_constant<int, 1>{}), acc, lane,
         [&](auto ph) __attribute__((always_inline)) { side(ic, std::integral_constant<int, 0>{}, ph); },
