@@ -1295,11 +1295,8 @@ constexpr int kWChunk = 2048;   // samples per chunk
 // than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
 // (N = 160: dir_linear's 128 rows + the density head's, the tile-major training path only)
 static inline bool wgrad_whole_tile(int N, int K) { return (N == 256 || N == 160) && K == 256; }
-#ifndef NERF_WG_WHOLE_CLEN
-#define NERF_WG_WHOLE_CLEN (kWChunk / 2)
-#endif
 static inline int wgrad_chunk_len_big(int N, int K) {
-  if (wgrad_whole_tile(N, K)) return NERF_WG_WHOLE_CLEN;   // wgrad_bf256_kernel: one block per chunk, 256 per step
+  if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
   if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
                                                     // 3 % faster but doubled the reduction)
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
@@ -1309,8 +1306,7 @@ static inline int wgrad_chunk_len_big(int N, int K) {
 // there are >= 256 chunks: 4,096 rays in 1,024-row chunks ran 8 blocks, 80-100 us per launch.
 static inline int wgrad_chunk_len(int N, int K, int64_t M) {
   int c = wgrad_chunk_len_big(N, K);
-  const int64_t min_chunks = wgrad_whole_tile(N, K) ? 256 * (kWChunk / 2) / NERF_WG_WHOLE_CLEN : 256;
-  while (c > 16 && (M + c - 1) / c < min_chunks) c /= 2;
+  while (c > 16 && (M + c - 1) / c < 256) c /= 2;
   return c;
 }
 
@@ -2087,175 +2083,6 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a once
 }
 
-// The same whole-tile GEMM with both operands staged sample-major and read back transposed
-// (`ds_read_b64_tr_b16`).  A 16-sample stage of a (and of x) is 16 rows of 256 features in the
-// tile-major rows: lane l of wave w loads features 4l .. 4l+3 of samples 4w .. 4w+3, one
-// `buffer_load_dwordx4` each (8 per lane per stage against the dword loader's 32), splits them into
-// three bf16 parts and writes each part's 4 values as one 8-byte LDS store into a [sample][feature]
-// image.  The MFMA fragments (8 consecutive samples of one feature per lane) come back by two
-// transposed reads each.  Image rows are 288 bf16 (576 B = 16 dwords mod 64): a 32-lane half's two
-// 4 x 16 blocks then fall on 64 distinct banks, and the stores are contiguous per row.  Every wave
-// still owns 64 columns (its x fragments) and all 32 NRT rows (the a fragments); the bias column is
-// summed per lane over its 4 samples of each stage, in double, and the 4 waves' sums are added in
-// wave order at the end.
-constexpr int kTrRow = 288;
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ bf16x4 lds_read_tr(const __bf16* p) {
-  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                        (__attribute__((address_space(3))) s16x4*)(const_cast<__bf16*>(p))));
-}
-__device__ __forceinline__ void split3_bf16x4(const f32x4& v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const __bf16 h0 = (__bf16)v[j];
-    const float r1 = v[j] - (float)h0;
-    const __bf16 h1 = (__bf16)r1;
-    p0[j] = h0;
-    p1[j] = h1;
-    p2[j] = (__bf16)(r1 - (float)h1);
-  }
-}
-template <int NRT = 8>
-__global__ void __launch_bounds__(256, 1)
-wgrad_tr256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                   int clen, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) __bf16 Img[2][2][3][kBfStage][kTrRow];   // [buffer][a | x][part][sample][feature]
-  const int chunk = blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wk = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, c = lane & 31;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const uint32_t lvo = 4u * (uint32_t)((lane >> 1) * 256 + 4 * (lane & 1));   // features 4l .. 4l+3 of a sample
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  f32x4 ra[4][4], rx[4][4];          // four stages of raw operands: [set][sample 4 wk + i]
-  double bacc[4] = {0.0, 0.0, 0.0, 0.0};
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;   // past the chunk: an empty resource, the loads read zeros
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      ra[SET][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ares, (int)lvo, (4 * wk + i) * 32, kRowLoadAux));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      rx[SET][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, (int)lvo, (4 * wk + i) * 32, kRowLoadAux));
-  };
-  auto split = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bacc[e] += (double)ra[SET][i][e];
-      bf16x4 p[3], q[3];
-      split3_bf16x4(ra[SET][i], p[0], p[1], p[2]);
-      split3_bf16x4(rx[SET][i], q[0], q[1], q[2]);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        *reinterpret_cast<bf16x4*>(&Img[buf][0][k][4 * wk + i][4 * lane]) = p[k];
-        *reinterpret_cast<bf16x4*>(&Img[buf][1][k][4 * wk + i][4 * lane]) = q[k];
-      }
-    }
-  };
-  // fragment of 8 samples (8h ..) of feature col0 + (lane & 31): two 4 x 16 transposed blocks
-  const int trow = 8 * h + ((lane & 15) >> 2), tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  auto frag = [&](int buf, int op, int part, int col0) __attribute__((always_inline)) {
-    const __bf16* p = &Img[buf][op][part][trow][col0 + tcol];
-    const bf16x4 lo = lds_read_tr(p), hi = lds_read_tr(p + 4 * kTrRow);
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  f32x16 acc[NRT][2];
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;   // a multiple of 4; extras read zeros
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using C2 = std::integral_constant<int, 2>;
-  load(C0{}, 0);
-  load(C1{}, 1);
-  load(C2{}, 2);
-  split(C0{}, 0);
-  __syncthreads();
-  // iteration st (set st % 4, buffer st % 2): stage st+3's loads; stage st's MFMAs with stage st+1's
-  // split in their shadow; barrier
-  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value, FB = SET & 1;
-    using Nxt = std::integral_constant<int, (SET + 1) & 3>;
-    using Ld = std::integral_constant<int, (SET + 3) & 3>;
-    load(Ld{}, st + 3);
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 fx[2][3];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fx[j][p] = frag(FB, 1, p, 64 * wk + 32 * j);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      bf16x8 fa[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = frag(FB, 0, p, 32 * i);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma_bf16(fa[0], fx[j][2], t);
-        t = mfma_bf16(fa[1], fx[j][1], t);
-        t = mfma_bf16(fa[2], fx[j][0], t);
-        t = mfma_bf16(fa[0], fx[j][1], t);
-        t = mfma_bf16(fa[1], fx[j][0], t);
-        acc[i][j] = mfma_bf16(fa[0], fx[j][0], t);
-      }
-    }
-    split(Nxt{}, FB ^ 1);
-    // schedule: the x fragments' reads, then per row tile its 6 reads and 12 MFMAs, each followed by
-    // VALU of the next stage's split; the split's LDS stores last
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 3, 0);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x200, 24, 0);
-    __syncthreads();
-  };
-  for (int st = 0; st < nstages; st += 4) {
-    iteration(C0{}, st);
-    iteration(C1{}, st + 1);
-    iteration(C2{}, st + 2);
-    iteration(std::integral_constant<int, 3>{}, st + 3);
-  }
-  constexpr int KP = kWT + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(32 * NRT, kWT);
-#pragma unroll
-  for (int i = 0; i < NRT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-    }
-  // bias column: the 4 waves' per-lane sums, added in wave order (the images are free after the loop's
-  // last barrier)
-  double* bsum = reinterpret_cast<double*>(&Img[0][0][0][0][0]);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) bsum[wk * kWT + 4 * lane + e] = bacc[e];
-  __syncthreads();
-  if (tid < 32 * NRT)
-    out[(size_t)tid * KP + kWT] = (float)(((bsum[tid] + bsum[kWT + tid]) + bsum[2 * kWT + tid]) + bsum[3 * kWT + tid]);
-}
-
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2508,20 +2335,11 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-#ifdef NERF_WG_TR
-      hipLaunchKernelGGL((wgrad_tr256_kernel<5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-#else
       hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                          ws);
-#endif
       rc = check_launch("wgrad_bf256w_kernel<5>");
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
-#if defined(NERF_WG_TR)
-      if (tiled)
-        hipLaunchKernelGGL(wgrad_tr256_kernel<8>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-      else
-        hipLaunchKernelGGL(wgrad_bf256w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-#elif !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
+#if !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
       if (tiled)
         hipLaunchKernelGGL(wgrad_bf256w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
       else
