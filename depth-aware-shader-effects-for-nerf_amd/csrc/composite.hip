@@ -14,67 +14,128 @@
 // per-sample tensor is empty and both maps are 0.
 //
 // Bound: HBM.  Reads 20 B/sample (rgb 12, sigma 4, z 4), writes 16 B/ray (+4 B/sample of
-// weights when requested).  Consecutive lanes touch consecutive samples of one ray.
+// weights when requested).
+//
+// Layout of the work: 16 lanes (one DPP row) per ray, 4 rays per wave.  A ray is taken in rounds
+// of 64 samples; in a round lane k owns samples 4k .. 4k+3 (contiguous: 16-byte loads of z, sigma
+// and the 48 bytes of rgb when the buffers allow, one 16-byte store of weights).  Per round: the
+// lane's product of its 4 factors, an exclusive product scan over the row's 16 lanes in double
+// (4 `row_shr` DPP steps, no LDS), each sample's T = carry * row prefix * lane prefix (products in
+// double, rounded once to float), and the lane's running sums.  The row's last lane carries the
+// product into the next round; the sums are added over the row by 4 DPP steps at the end.  (One
+// wave per ray with 64-lane shuffle scans and reductions through ds_bpermute ran 0.50 / 0.88 ms for
+// the 800^2 coarse / fine composite, 0.28 of HBM bandwidth: it was bound by the cross-lane traffic.)
 #include "common.h"
 
 namespace nerf {
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+// v from the lane `off` below in the same 16-lane row; lanes below off get `fill`
+template <int OFF>
+__device__ __forceinline__ double row_shr(double v, double fill) {
+  const long long b = __builtin_bit_cast(long long, v), fb = __builtin_bit_cast(long long, fill);
+  const int lo = __builtin_amdgcn_update_dpp((int)fb, (int)b, 0x110 + OFF, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(fb >> 32), (int)(b >> 32), 0x110 + OFF, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// inclusive product / sum over lanes 0..k of the row
+__device__ __forceinline__ double row_scan_mul(double v) {
+  v *= row_shr<1>(v, 1.0);
+  v *= row_shr<2>(v, 1.0);
+  v *= row_shr<4>(v, 1.0);
+  v *= row_shr<8>(v, 1.0);
+  return v;
+}
+__device__ __forceinline__ double row_scan_add(double v) {
+  v += row_shr<1>(v, 0.0);
+  v += row_shr<2>(v, 0.0);
+  v += row_shr<4>(v, 0.0);
+  v += row_shr<8>(v, 0.0);
   return v;
 }
 
+// VEC: every pointer 16-byte aligned and N % 4 == 0, so a lane's 4 samples load as one f32x4
+template <bool VEC>
 __global__ void __launch_bounds__(256)
 composite_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma, const float* __restrict__ zv,
                  int64_t B, int N, float* __restrict__ rgb_map, float* __restrict__ depth_map,
                  float* __restrict__ weights) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= B) return;
-  const int64_t base = r * N;
+  const int k = threadIdx.x & 15;
+  const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool ray = r < B;          // rows past B run on with no samples (the DPP stays inside a row)
+  const int64_t base = ray ? r * N : 0;
+  if (ray && N == 1 && weights && k == 0) weights[base] = 0.0f;
+  const int n_eff = ray && N > 1 ? N : 0;
   double carry = 1.0;
   double acc_r = 0.0, acc_g = 0.0, acc_b = 0.0, acc_wz = 0.0, acc_w = 0.0;
-  if (N == 1 && weights && lane == 0) weights[base] = 0.0f;
-  const int n_eff = N > 1 ? N : 0;
   for (int c0 = 0; c0 < n_eff; c0 += 64) {
-    const int s = c0 + lane;
-    const bool valid = s < N;
-    float alpha = 0.0f, z = 0.0f;
-    double f = 1.0;
-    if (valid) {
-      z = zv[base + s];
-      const float dist = (s + 1 < N) ? zv[base + s + 1] - z : 1e-3f;
-      alpha = 1.0f - expf_rn(-sigma[base + s] * dist);
-      f = (double)((1.0f - alpha) + 1e-10f);
-    }
-    double incl = f;
+    const int s0 = c0 + 4 * k;
+    float z[5], sg[4], c[12];
+    if (VEC && s0 + 4 <= n_eff) {
+      const f32x4 zq = *reinterpret_cast<const f32x4*>(zv + base + s0);
+      const f32x4 sq = *reinterpret_cast<const f32x4*>(sigma + base + s0);
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double up = __shfl_up(incl, off);
-      if (lane >= off) incl *= up;
+      for (int j = 0; j < 4; ++j) z[j] = zq[j], sg[j] = sq[j];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const f32x4 cq = *reinterpret_cast<const f32x4*>(rgb + 3 * (base + s0) + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[4 * q + j] = cq[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool v = s0 + j < n_eff;
+        z[j] = v ? zv[base + s0 + j] : 0.0f;
+        sg[j] = v ? sigma[base + s0 + j] : 0.0f;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) c[3 * j + q] = v ? rgb[3 * (base + s0 + j) + q] : 0.0f;
+      }
     }
-    double excl = __shfl_up(incl, 1);
-    if (lane == 0) excl = 1.0;
-    const float T = (float)(carry * excl);
-    carry *= __shfl(incl, 63);
-    if (valid) {
-      const float w = alpha * T;
-      if (weights) weights[base + s] = w;
-      const int64_t e = 3 * (base + s);
-      acc_r += (double)(w * rgb[e]);
-      acc_g += (double)(w * rgb[e + 1]);
-      acc_b += (double)(w * rgb[e + 2]);
-      acc_wz += (double)(w * z);
-      acc_w += (double)w;
+    z[4] = s0 + 4 < n_eff ? zv[base + s0 + 4] : 0.0f;
+    float alpha[4];
+    double f[4], lane_prod = 1.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = s0 + j;
+      alpha[j] = 0.0f;
+      f[j] = 1.0;
+      if (s < n_eff) {
+        const float dist = (s + 1 < N) ? z[j + 1] - z[j] : 1e-3f;
+        alpha[j] = 1.0f - expf_rn(-sg[j] * dist);
+        f[j] = (double)((1.0f - alpha[j]) + 1e-10f);
+      }
+      lane_prod *= f[j];
+    }
+    const double incl = row_scan_mul(lane_prod);
+    double pre = carry * row_shr<1>(incl, 1.0);      // product of every factor before this lane's first
+    carry *= __shfl(incl, 15, 16);
+    float w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = alpha[j] * (float)pre;                  // 0 past the ray's end (alpha = 0)
+      pre *= f[j];
+      acc_r += (double)(w[j] * c[3 * j]);
+      acc_g += (double)(w[j] * c[3 * j + 1]);
+      acc_b += (double)(w[j] * c[3 * j + 2]);
+      acc_wz += (double)(w[j] * z[j]);
+      acc_w += (double)w[j];
+    }
+    if (weights) {
+      if (VEC && s0 + 4 <= n_eff) {
+        *reinterpret_cast<f32x4*>(weights + base + s0) = f32x4{w[0], w[1], w[2], w[3]};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (s0 + j < n_eff) weights[base + s0 + j] = w[j];
+      }
     }
   }
-  acc_r = wave_sum(acc_r);
-  acc_g = wave_sum(acc_g);
-  acc_b = wave_sum(acc_b);
-  acc_wz = wave_sum(acc_wz);
-  acc_w = wave_sum(acc_w);
-  if (lane == 0) {
+  acc_r = row_scan_add(acc_r);
+  acc_g = row_scan_add(acc_g);
+  acc_b = row_scan_add(acc_b);
+  acc_wz = row_scan_add(acc_wz);
+  acc_w = row_scan_add(acc_w);
+  if (ray && k == 15) {
     rgb_map[3 * r] = (float)acc_r;
     rgb_map[3 * r + 1] = (float)acc_g;
     rgb_map[3 * r + 2] = (float)acc_b;
@@ -85,8 +146,13 @@ composite_kernel(const float* __restrict__ rgb, const float* __restrict__ sigma,
 int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N, float* rgb_map,
                      float* depth, float* weights, hipStream_t s) {
   if (B == 0) return NERF_OK;
-  hipLaunchKernelGGL(composite_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, rgb, sigma, z, B, N,
-                     rgb_map, depth, weights);
+  const bool vec = N % 4 == 0 && (uintptr_t)rgb % 16 == 0 && (uintptr_t)sigma % 16 == 0 && (uintptr_t)z % 16 == 0 &&
+                   (!weights || (uintptr_t)weights % 16 == 0);
+  const dim3 grid((unsigned)((B + 15) / 16));
+  if (vec)
+    hipLaunchKernelGGL(composite_kernel<true>, grid, dim3(256), 0, s, rgb, sigma, z, B, N, rgb_map, depth, weights);
+  else
+    hipLaunchKernelGGL(composite_kernel<false>, grid, dim3(256), 0, s, rgb, sigma, z, B, N, rgb_map, depth, weights);
   return check_launch("composite_kernel");
 }
 

@@ -166,14 +166,20 @@ def test_composite_kernel(ref_state):
     from nerfmi import _lib
     lib = _lib.load()
     torch.manual_seed(8)
-    for B, N in ((37, 64), (5, 192), (9, 1), (3, 100), (2, 1000)):
+
+    def unaligned(t):   # the same values at a 4-byte offset from a 16-byte boundary (the scalar-load kernel)
+        buf = torch.empty(t.numel() + 1, device="cuda")
+        buf[1:] = t.reshape(-1).cuda()
+        return buf[1:].view(t.shape)
+    for B, N, odd in ((37, 64, False), (5, 192, False), (9, 1, False), (3, 100, False), (2, 1000, False),
+                      (4, 2, False), (6, 7, False), (19, 17, False), (21, 64, True), (3, 192, True)):
         z = torch.sort(torch.rand(B, N) * 4 + 2, dim=-1).values
         sigma = torch.relu(torch.randn(B, N) * 3)
         rgb = torch.rand(B, N, 3)
-        zc, sc, rc = z.cuda(), sigma.cuda(), rgb.cuda()
+        zc, sc, rc = (unaligned(t) if odd else t.cuda() for t in (z, sigma, rgb))
         rm = torch.empty(B, 3, device="cuda")
         dm = torch.empty(B, device="cuda")
-        wm = torch.empty(B, N, device="cuda")
+        wm = unaligned(torch.zeros(B, N)) if odd else torch.empty(B, N, device="cuda")
         _lib.check(lib.nerf_composite(_lib.ptr(rc), _lib.ptr(sc), _lib.ptr(zc), B, N, _lib.ptr(rm), _lib.ptr(dm),
                                       _lib.ptr(wm), _lib.stream()), "composite")
         r_ref, d_ref, w_ref = O.composite(rgb, sigma[..., None], z)
