@@ -571,8 +571,8 @@ __device__ __forceinline__ f32x16 mfma16t(u32x4 a, h16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h16x8, a), b, c, 0, 0, 0);
 }
 
-// Split tiles 0..NT-1 of X (k-steps 2t + s: accumulator elements 8s..8s+7) at the sample's scale;
-// returns 1 / s_g.
+// Split tiles 0..NT-1 of X (k-steps 2t + s: accumulator elements 8s..8s+7) at the sample's scale,
+// negative for odd samples (lane & 1; see mlp_backward16_bound_kernel); returns 1 / s_g.
 template <int NT>
 __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16], h16x8 (&bl)[16]) {
   float m = 0.0f;
@@ -583,7 +583,8 @@ __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16
   m = fmaxf(m, __shfl_xor(m, 32));
   int E = (int)((__float_as_uint(m) >> 23) & 0xffu);
   E = E < 14 ? 14 : E;
-  const float sc = __uint_as_float((uint32_t)(267 - E) << 23);
+  const float sgn = (threadIdx.x & 1) ? -1.0f : 1.0f;
+  const float sc = sgn * __uint_as_float((uint32_t)(267 - E) << 23);
   typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -599,7 +600,7 @@ __device__ __forceinline__ float split_rows(const f32x16 (&X)[8], h16x8 (&bh)[16
         bl[2 * t + q][j] = lo2[0];
         bl[2 * t + q][j + 1] = lo2[1];
       }
-  return __uint_as_float((uint32_t)(E - 13) << 23);
+  return sgn * __uint_as_float((uint32_t)(E - 13) << 23);
 }
 
 // out (8 tiles) = (W^T g) from the split operands of KS k-steps; inv_w = 1/s_w, inv_g = 1/s_g.
@@ -1137,7 +1138,14 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
       }
   }
   m_dir = sample_max(m_dir);
-  const float s_dir = pow2_scale(m_dir);
+  // Every split scale carries the sample's sign sgn (odd samples negative).  The MFMA unit's f32
+  // accumulation of f16 products is not correctly rounded and its error leans negative (-0.12 ulp
+  // on average, profiles/r04/mfma_f16_accumulation_rounding.log); a gradient row of an odd sample is
+  // computed negated, so its rounding error comes back with the opposite sign, and the per-column
+  // errors cancel in the sums over samples that make the weight and bias gradients instead of adding
+  // up.  (Each row's own error is unchanged; the sign is exact: the scales stay powers of two.)
+  const float sgn = (lane & 1) ? -1.0f : 1.0f;
+  const float s_dir = sgn * pow2_scale(m_dir);
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1145,7 +1153,7 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
 #pragma unroll
       for (int e = 0; e < 4; ++e) split_into(dhd[t][4 * q + e] * s_dir, in[8 + 2 * t + q / 2], 4 * (q & 1) + e);
   // d pre_7's scale: |W_dh^T g + dsigma w_sigma| <= C_dir max|g| + |dsigma| max|w_sigma|
-  float s_cur = pow2_scale(cst[kT16C + 7] * m_dir + fabsf(dsp) * cst[kT16WsigMax]);
+  float s_cur = sgn * pow2_scale(cst[kT16C + 7] * m_dir + fabsf(dsp) * cst[kT16WsigMax]);
   float inv_prev = cst[kT16InvS + 7] / s_dir;
 
   // the weight stream: W^T fragments of dir_linear's h-part, then trunk layers 7 .. 1
@@ -1225,7 +1233,7 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
                                            });
     // the inputs of this layer are complete: the scale of d pre_{l-1} from the bound
     m = sample_max(m);
-    s_nxt = pow2_scale(cst[kT16C + l - 1] * m);
+    s_nxt = sgn * pow2_scale(cst[kT16C + l - 1] * m);
     m = 0.0f;
     if constexpr (last) {
       run_group<1, 8, 0, 0, kSideCur, true>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
