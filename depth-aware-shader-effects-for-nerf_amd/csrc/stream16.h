@@ -50,9 +50,14 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // ds_*_addtid or GWS): the generated code's only M0 writes are these (checked in the .s; the
 // Makefile silences the warning for this file).
 // lds_base: the ring's LDS byte address + 1024 * wave (this wave's first piece).
+// Timing-only ablation builds (results are wrong; scripts/ab_bench.sh): NERF16_ABL_NO_DMA drops the
+// weight stream's LDS-DMA, NERF16_ABL_NO_DSREAD its fragment reads, NERF16_ABL_NO_SIDE the side work.
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
                                                 uint32_t voff) {
+#ifdef NERF16_ABL_NO_DMA
+  return;
+#endif
   const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
 #ifdef NERF16_M0_SAVE
   uint32_t keep;
@@ -93,6 +98,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 // A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
 template <int KK>
 __device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
+#ifdef NERF16_ABL_NO_DSREAD
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int part = 0; part < 2; ++part) asm volatile("" : "+v"(a[ti][part]));
+  return;
+#endif
 #pragma unroll
   for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
@@ -154,11 +166,15 @@ __device__ __forceinline__ void half_step(const h16x8 (&am)[4][2], const Operand
                                           Hook&& hook) {
   // the side work's small LDS reads (bias, density weights) go first: LDS returns in order, so its
   // VALU then waits for them alone, not for the fragment reads issued after them
+#ifndef NERF16_ABL_NO_SIDE
   side(std::integral_constant<int, 0>{});
+#endif
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (READ) read_kstep<KK_R>(slot_r, ar, lane);
   mfma_kstep<G, FIRST>(am, b, acc, hook);
+#ifndef NERF16_ABL_NO_SIDE
   side(std::integral_constant<int, 1>{});
+#endif
 #ifndef NERF16_DSR_PER_GAP
 #define NERF16_DSR_PER_GAP 1
 #endif
