@@ -233,10 +233,6 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_sched_barrier(0);
   const float* stream = packed + kOff16;
-#ifdef NERF16_ABL_NO_DMA   // (timing-only: finite stand-in weights)
-  for (int i = threadIdx.x; i < 4 * kChunkFloats; i += 64 * kW16Waves) lds[i] = 0.0f;
-  __syncthreads();
-#endif
   const uint32_t lds_dma = (uint32_t)(uintptr_t)(lptr_t)lds + 1024u * wave;   // this wave's first piece
   const uint32_t voff = 16u * lane + 1024u * wave;
   chunk_dma<0>(stream, 0, lds_dma, voff);
@@ -284,14 +280,17 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   wait_vmcnt<8>();                                          // this wave's part of chunk 0 (chunks 1-2 in flight)
   __builtin_amdgcn_s_barrier();
-#if defined(NERF16_ABL_NO_DSREAD) || defined(NERF16_ABL_NO_SIDE)   // (timing-only: finite stand-ins)
-  h16x8 a0[4][2] = {}, a1[4][2] = {};
+  h16x8 a0[4][2], a1[4][2];
+#ifdef NERF16_ABL_NO_SIDE    // (timing-only: finite stand-in operands)
   Operand in[16] = {};
 #else
-  h16x8 a0[4][2], a1[4][2];
   Operand in[16];
 #endif
   read_kstep<0>(lds, a0, lane);
+#ifdef NERF16_ABL_NO_DSREAD  // (timing-only: real fragments of chunk 0, kept for the whole stream)
+  read_kstep_lds<0>(lds, a0, lane);
+  read_kstep_lds<1>(lds, a1, lane);
+#endif
 
   f32x16 acc[8];
   float m = 0.0f, part = 0.0f;

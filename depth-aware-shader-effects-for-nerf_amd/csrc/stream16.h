@@ -55,8 +55,8 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 template <int SLOT, int I>
 __device__ __forceinline__ void chunk_dma_piece(const float* __restrict__ stream, int c, uint32_t lds_base,
                                                 uint32_t voff) {
-#ifdef NERF16_ABL_NO_DMA
-  return;
+#ifdef NERF16_ABL_NO_DMA   // the ring keeps chunks 0-3: real weights, never refreshed
+  if (c >= 4) return;
 #endif
   const char* src = reinterpret_cast<const char*>(stream) + (size_t)c * (kChunkFloats * 4);
 #ifdef NERF16_M0_SAVE
@@ -97,20 +97,24 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // A fragments (4 tiles x {hi, lo}) of k-step KK of the chunk in `slot`.
 template <int KK>
-__device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
-#ifdef NERF16_ABL_NO_DSREAD
-#pragma unroll
-  for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-    for (int part = 0; part < 2; ++part) asm volatile("" : "+v"(a[ti][part]));
-  return;
-#endif
+__device__ __forceinline__ void read_kstep_lds(const float* slot, h16x8 (&a)[4][2], int lane) {
 #pragma unroll
   for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
     for (int part = 0; part < 2; ++part)
       a[ti][part] = __builtin_bit_cast(
           h16x8, *reinterpret_cast<const f32x4*>(slot + ((KK * 4 + ti) * 2 + part) * 256 + lane * 4));
+}
+template <int KK>
+__device__ __forceinline__ void read_kstep(const float* slot, h16x8 (&a)[4][2], int lane) {
+#ifdef NERF16_ABL_NO_DSREAD   // the registers keep the prologue's real fragments
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int part = 0; part < 2; ++part) asm volatile("" : "+v"(a[ti][part]));
+  return;
+#endif
+  read_kstep_lds<KK>(slot, a, lane);
 }
 
 // One k-step of group G (tiles 4G .. 4G+3).

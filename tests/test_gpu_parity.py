@@ -261,6 +261,47 @@ def test_sample_importance_shapes_vs_oracle(nerfmi_mod):
         assert torch.equal(pts.cpu(), pts_ref), (B, N, Nf)
 
 
+def test_sample_importance_merge_scatter(nerfmi_mod):
+    """nerf_sample_importance_merge: z_all equals the resample alone, every coarse (rgb, sigma) sits at
+    the merged slot of its z, and each fine sample's slot holds its z (ragged, N = 1, and the largest
+    supported N and Nf)."""
+    import ctypes
+    from nerfmi import _lib
+    lib = _lib.load()
+    torch.manual_seed(13)
+    for B, N, Nf in ((33, 64, 128), (5, 7, 9), (6, 64, 512), (3, 256, 1024), (4, 1, 16)):
+        z = torch.sort(torch.rand(B, N) * 4 + 2, dim=-1).values
+        w = torch.rand(B, N) * (torch.rand(B, N) > 0.5)
+        u = torch.rand(B, Nf)
+        u_lin = torch.linspace(0, 1, Nf + 1)[:-1].contiguous()
+        rgb_c, sigma_c = torch.rand(B, N, 3), torch.rand(B, N)
+        T = N + Nf
+        zg, wg, ug, ul, rc, sc = (t.cuda() for t in (z, w, u, u_lin, rgb_c, sigma_c))
+        z_all = torch.empty(B, T, device="cuda")
+        rgb_all = torch.full((B, T, 3), float("nan"), device="cuda")
+        sigma_all = torch.full((B, T), float("nan"), device="cuda")
+        z_fine = torch.empty(B, Nf, device="cuda")
+        slot = torch.empty(B, Nf, dtype=torch.int32, device="cuda")
+        _lib.check(lib.nerf_sample_importance_merge(
+            _lib.ptr(zg), _lib.ptr(wg), _lib.ptr(rc), _lib.ptr(sc), B, N, Nf, _lib.ptr(ul), _lib.ptr(ug),
+            ctypes.c_uint64(0), _lib.ptr(z_all), _lib.ptr(rgb_all), _lib.ptr(sigma_all), _lib.ptr(z_fine),
+            _lib.ptr(slot), _lib.stream()), "importance_merge")
+        torch.cuda.synchronize()
+        z_ref, _ = O.sample_importance_h1(torch.zeros(B, 3), torch.zeros(B, 3), z, w, Nf, u)
+        assert torch.equal(z_all.cpu(), z_ref), (B, N, Nf)
+        za, ra, sa, zf, sl = (t.cpu() for t in (z_all, rgb_all, sigma_all, z_fine, slot))
+        rows = torch.arange(B)[:, None]
+        assert torch.equal(za[rows, sl.long()], zf), (B, N, Nf)          # fine z at its slot
+        fine = torch.zeros(B, T, dtype=torch.bool)
+        fine[rows, sl.long()] = True
+        assert int(fine.sum()) == B * Nf                                  # distinct slots
+        assert torch.equal(torch.sort(za[~fine].reshape(B, N), dim=-1).values, z)   # the coarse z fill the rest
+        # coarse slots carry the coarse evaluation of their z (ties between equal coarse z aside, the
+        # k-th coarse slot in order holds coarse sample k)
+        assert torch.equal(ra[~fine].reshape(B, N, 3), rgb_c), (B, N, Nf)
+        assert torch.equal(sa[~fine].reshape(B, N), sigma_c), (B, N, Nf)
+
+
 def test_hierarchical_h1(nerfmi_mod, model, golden, golden_meta, app_vec):
     f6 = golden("f6_hierarchical.npz")
     m = golden_meta["F6"]
