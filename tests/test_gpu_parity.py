@@ -343,6 +343,30 @@ def test_edge_sizes(nerfmi_mod, model, ref_state, app_vec):
     assert rgb.shape == (4, 5, 3) and depth.shape == (4, 5, 1)
 
 
+def test_hierarchical_extreme_sizes(nerfmi_mod, model, ref_state, app_vec, golden):
+    """The largest supported hierarchical pass (N = 256, Nf = 1024: 1,280 merged samples per ray) and
+    ragged ones (samples per ray not a multiple of a wave's 32, one fine sample): the coarse maps
+    against the oracle, and the fine maps with the fine samples held equal (the oracle's fine pass on
+    the GPU's merged z, as in test_full_frame_properties)."""
+    o, d = crop(golden, "chair", 24)
+    torch.manual_seed(14)
+    for N, Nf in ((256, 1024), (50, 70), (33, 1), (7, 200)):
+        u = torch.rand(o.shape[0], Nf)
+        rgb, depth, ex = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, N, Nf,
+                                                appearance_embedding=app_vec.cuda(), perturb=False,
+                                                hierarchical=True, u_rand=u)
+        r_ref, _, ex_ref = O.render_rays_h1(ref_state, o, d, 2.0, 6.0, N, Nf, app_vec, None, u)
+        close(ex["rgb_map_coarse"], ex_ref["rgb_map_coarse"], what=f"coarse rgb N={N} Nf={Nf}")
+        close(ex["depth_map_coarse"], ex_ref["depth_map_coarse"], what=f"coarse depth N={N} Nf={Nf}")
+        z = ex["z_vals"].cpu()
+        assert z.shape == (o.shape[0], N + Nf) and bool((z[:, 1:] >= z[:, :-1]).all())
+        dn = O.normalize(d)
+        pts = o[:, None, :] + dn[:, None, :] * z[..., None]
+        r_fix, d_fix, _ = O._pass(ref_state, pts, dn, z, app_vec)
+        close(rgb, r_fix, what=f"fine rgb, same z, N={N} Nf={Nf}")
+        close(depth, d_fix, what=f"fine depth, same z, N={N} Nf={Nf}")
+
+
 def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_meta, arith):
     """800x800 hierarchical 64+128 (the bench workload): size-independent properties on every ray,
     and accuracy on 4096 rays sampled across the frame.
