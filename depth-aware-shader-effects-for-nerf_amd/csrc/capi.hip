@@ -417,13 +417,13 @@ int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, in
 
 // Workspace carve of nerf_render_rays, in this order (each region 256-B aligned), T = N + Nf:
 //   dirs (B,3) | z (B,N) | feat (B,256) | rgb_c (B,N,3) | sigma_c (B,N) | w_c (B,N) | z_all (B,T)
-//   | z_fine (B,Nf) | fine_slot (B,Nf) int32 | rgb_all (B,T,3) | sigma_all (B,T) | maps (B,4)
-enum { W_DIRS, W_Z, W_FEAT, W_RGBC, W_SIGC, W_WC, W_ZALL, W_ZF, W_SLOT, W_RGBA, W_SIGA, W_MAPS, W_COUNT };
+//   | z_fine (B,Nf) | merged_src (B,T) uint16 | rgb_f (B,Nf,3) | sigma_f (B,Nf) | maps (B,4)
+enum { W_DIRS, W_Z, W_FEAT, W_RGBC, W_SIGC, W_WC, W_ZALL, W_ZF, W_SRC, W_RGBF, W_SIGF, W_MAPS, W_COUNT };
 
 static size_t carve(int64_t B, int N, int Nf, size_t* off) {
   const size_t T = (size_t)N + Nf, b = (size_t)B;
   const size_t sizes[W_COUNT] = {b * 3, b * N, b * kRayFeat, b * N * 3, b * N, b * N, b * T,
-                                 b * Nf, b * Nf, b * T * 3, b * T, b * 4};
+                                 b * Nf, (b * T + 1) / 2, b * Nf * 3, b * Nf, b * 4};
   size_t at = 0;
   for (int i = 0; i < W_COUNT; ++i) {
     off[i] = at;
@@ -483,18 +483,21 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   float* crgb = coarse_rgb ? coarse_rgb : maps;
   float* cdepth = coarse_depth ? coarse_depth : maps + 3 * B;
   if ((rc = launch_composite(rgb_c, sigma_c, z, B, N, crgb, cdepth, wc, s))) return rc;
-  // H1 fine pass: resample + merge, coarse evaluations reused at their merged slots, the MLP run on
-  // the Nf new samples only, composite over all N+Nf.
-  const int T = N + Nf;
+  // H1 fine pass: resample + merge (each merged slot records which coarse or fine sample it holds),
+  // the MLP run on the Nf new samples only, in sample order, and the composite over all N+Nf merged
+  // samples gathering the coarse evaluations and the fine ones through the map.  (Round 3 scattered
+  // the coarse results into merged rows and the fine MLP wrote into its slots: 4.0 GB written by
+  // the resample and 24 B per fine sample by the MLP, for the same bits.)
   float* z_fine = region(W_ZF);
-  int* slot = (int*)region(W_SLOT);
-  float* rgb_all = region(W_RGBA);
-  float* sigma_all = region(W_SIGA);
-  if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed_f, z_all,
-                              nullptr, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, slot, s)))
+  uint16_t* msrc = (uint16_t*)region(W_SRC);
+  float* rgb_f = region(W_RGBF);
+  float* sigma_f = region(W_SIGF);
+  if ((rc = launch_importance(nullptr, nullptr, z, wc, B, N, Nf, u_lin, u_rand, seed_f, z_all, nullptr, nullptr,
+                              nullptr, nullptr, nullptr, z_fine, nullptr, s, msrc)))
     return rc;
-  if ((rc = profiled_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_all, sigma_all, slot, T, s))) return rc;
-  return launch_composite(rgb_all, sigma_all, z_all, B, T, rgb_map, depth_map, weights_out, s);
+  if ((rc = profiled_mlp(packed, rays_o, dn, z_fine, B, Nf, feat, rgb_f, sigma_f, nullptr, 0, s))) return rc;
+  return launch_composite_merged(rgb_c, sigma_c, rgb_f, sigma_f, msrc, z_all, B, N, Nf, rgb_map, depth_map,
+                                 weights_out, s);
 }
 
 }  // extern "C"

@@ -114,7 +114,8 @@ int launch_stratified(const float* o, const float* d, int64_t B, float near_f, f
 int launch_importance(const float* o, const float* d, const float* z, const float* w,
                       int64_t B, int N, int Nf, const float* u_lin, const float* u_rand,
                       uint64_t seed, float* z_all, float* pts_all, const float* rgb_c, const float* sigma_c,
-                      float* rgb_all, float* sigma_all, float* z_fine, int* fine_slot, hipStream_t s);
+                      float* rgb_all, float* sigma_all, float* z_fine, int* fine_slot, hipStream_t s,
+                      uint16_t* merged_src = nullptr);
 int launch_pack(const float* const* params, float* packed, hipStream_t s);
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
                         int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
@@ -127,5 +128,10 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
                hipStream_t s, float* save = nullptr, const float* encd = nullptr, uint32_t* masks = nullptr);
 int launch_composite(const float* rgb, const float* sigma, const float* z, int64_t B, int N,
                      float* rgb_map, float* depth, float* weights, hipStream_t s);
+// The fine composite of nerf_render_rays: merged slot p of ray r holds sample src[r T + p] of
+// cat[coarse (rgb_c, sigma_c: N per ray), fine (rgb_f, sigma_f: Nf per ray)], z_all its z.
+int launch_composite_merged(const float* rgb_c, const float* sigma_c, const float* rgb_f, const float* sigma_f,
+                            const uint16_t* src, const float* z_all, int64_t B, int N, int Nf, float* rgb_map,
+                            float* depth, float* weights, hipStream_t s);
 
 }  // namespace nerf

@@ -17,7 +17,10 @@
 //
 // Coarse-evaluation reuse (optional outputs): the kernel also scatters the coarse pass's
 // (rgb, sigma) into their merged slots and emits the fine samples with their slots, so the
-// fine MLP pass evaluates only the Nf new samples.  The MLP is deterministic per sample and a
+// fine MLP pass evaluates only the Nf new samples.  Or (merged_src, nerf_render_rays) it records
+// for each merged slot which sample sits there (index into cat[coarse, fine]) and emits the fine
+// samples alone: the fine MLP then writes its results in sample order and the composite gathers
+// through the map, so nothing is scattered.  The MLP is deterministic per sample and a
 // coarse sample's point o + d*z is recomputed bit-identically, so this equals re-evaluating all
 // N+Nf merged samples (tests/test_gpu_parity.py::test_coarse_reuse_is_bit_identical).
 //
@@ -58,7 +61,7 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
                   const float* __restrict__ u_rand, uint64_t seed, float* __restrict__ z_all,
                   float* __restrict__ pts_all, const float* __restrict__ rgb_c, const float* __restrict__ sigma_c,
                   float* __restrict__ rgb_all, float* __restrict__ sigma_all, float* __restrict__ z_fine,
-                  int* __restrict__ fine_slot) {
+                  int* __restrict__ fine_slot, uint16_t* __restrict__ merged_src) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -164,6 +167,7 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
       }
     }
     zo[pos] = v;
+    if (merged_src) merged_src[r * T + pos] = (uint16_t)e;
     if (coarse) {
       if (rgb_all) {                           // coarse evaluation reused at its merged slot
         const int64_t src = r * N + e, dst = r * T + pos;
@@ -174,7 +178,7 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
       }
     } else if (z_fine) {                       // fine sample to evaluate, and where its result goes
       z_fine[r * Nf + (e - N)] = v;
-      fine_slot[r * Nf + (e - N)] = pos;
+      if (fine_slot) fine_slot[r * Nf + (e - N)] = pos;
     }
     if (pts_all) {
       float* p = pts_all + 3 * (r * T + pos);
@@ -188,11 +192,12 @@ importance_kernel(const float* __restrict__ o, const float* __restrict__ d, cons
 int launch_importance(const float* o, const float* d, const float* z, const float* w, int64_t B, int N, int Nf,
                       const float* u_lin, const float* u_rand, uint64_t seed, float* z_all, float* pts_all,
                       const float* rgb_c, const float* sigma_c, float* rgb_all, float* sigma_all, float* z_fine,
-                      int* fine_slot, hipStream_t s) {
+                      int* fine_slot, hipStream_t s, uint16_t* merged_src) {
   if (B == 0) return NERF_OK;
   const size_t lds = (size_t)4 * ((N + 1) + 2 * N + Nf) * sizeof(float);
   hipLaunchKernelGGL(importance_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), lds, s, o, d, z, w, B, N, Nf,
-                     u_lin, u_rand, seed, z_all, pts_all, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, fine_slot);
+                     u_lin, u_rand, seed, z_all, pts_all, rgb_c, sigma_c, rgb_all, sigma_all, z_fine, fine_slot,
+                     merged_src);
   return check_launch("importance_kernel");
 }
 
