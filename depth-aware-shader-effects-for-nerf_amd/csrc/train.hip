@@ -2040,29 +2040,53 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     using FBn = std::integral_constant<int, FB ^ 1>;
     load(Ld{}, st + 3);
     __builtin_amdgcn_sched_barrier(0);
+#ifndef NERF_WG_FRAG_JIT
+    // row tile i's MFMAs run while tile i+1's 3 fragments are read (read just before its own MFMAs,
+    // each tile waited out the LDS latency: ~8 exposed waits per stage)
+    bf16x8 fa[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fa[0][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][c][8 * h]);
 #pragma unroll
     for (int i = 0; i < NRT; ++i) {
-      bf16x8 fa[3];
+      if (i + 1 < NRT) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * i + c][8 * h]);
+        for (int p = 0; p < 3; ++p)
+          fa[(i + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
+      }
+      const bf16x8 (&f)[3] = fa[i & 1];
+#else   // A/B: each tile's fragments read just before its MFMAs
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) {
+      bf16x8 f[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * i + c][8 * h]);
+#endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x16 t = acc[i][j];
-        t = mfma_bf16(fa[0], fx[FB][j][2], t);
-        t = mfma_bf16(fa[1], fx[FB][j][1], t);
-        t = mfma_bf16(fa[2], fx[FB][j][0], t);
-        t = mfma_bf16(fa[0], fx[FB][j][1], t);
-        t = mfma_bf16(fa[1], fx[FB][j][0], t);
-        acc[i][j] = mfma_bf16(fa[0], fx[FB][j][0], t);
+        t = mfma_bf16(f[0], fx[FB][j][2], t);
+        t = mfma_bf16(f[1], fx[FB][j][1], t);
+        t = mfma_bf16(f[2], fx[FB][j][0], t);
+        t = mfma_bf16(f[0], fx[FB][j][1], t);
+        t = mfma_bf16(f[1], fx[FB][j][0], t);
+        acc[i][j] = mfma_bf16(f[0], fx[FB][j][0], t);
       }
     }
     split_x(Nxt{}, FBn{});
     split_a(Nxt{}, FB ^ 1);
-    // schedule: per row tile its 3 fragment reads, then its 12 MFMAs each followed by 2 VALU of the
-    // next stage's splits; the split's LDS writes last
+    // schedule: per row tile 3 fragment reads (the next tile's, or this tile's under
+    // NERF_WG_FRAG_JIT), then its 12 MFMAs each followed by 2 VALU of the next stage's splits; the
+    // split's LDS writes last
+#ifndef NERF_WG_FRAG_JIT
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);         // tile 0's reads
+#endif
 #pragma unroll
     for (int i = 0; i < NRT; ++i) {
+#ifndef NERF_WG_FRAG_JIT
+      if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS reads (tile i+1)
+#else
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads
+#endif
 #pragma unroll
       for (int k = 0; k < 12; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
