@@ -2040,21 +2040,7 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     using FBn = std::integral_constant<int, FB ^ 1>;
     load(Ld{}, st + 3);
     __builtin_amdgcn_sched_barrier(0);
-#if defined(NERF_WG_AHEAD2)   // A/B: two tiles ahead, and VALU ahead of the stage's first MFMA
-    bf16x8 fa[3][3];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fa[t][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * t + c][8 * h]);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 2 < NRT) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fa[(i + 2) % 3][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * (i + 2) + c][8 * h]);
-      }
-      const bf16x8 (&f)[3] = fa[i % 3];
-#elif !defined(NERF_WG_FRAG_JIT)
+#ifndef NERF_WG_FRAG_JIT
     // row tile i's MFMAs run while tile i+1's 3 fragments are read (read just before its own MFMAs,
     // each tile waited out the LDS latency: ~8 exposed waits per stage)
     bf16x8 fa[2][3];
@@ -2091,17 +2077,12 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     // schedule: per row tile 3 fragment reads (the next tile's, or this tile's under
     // NERF_WG_FRAG_JIT), then its 12 MFMAs each followed by 2 VALU of the next stage's splits; the
     // split's LDS writes last
-#if defined(NERF_WG_AHEAD2)
-    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);         // tiles 0 and 1
-    __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);        // VALU while they land
-#elif !defined(NERF_WG_FRAG_JIT)
+#ifndef NERF_WG_FRAG_JIT
     __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);         // tile 0's reads
 #endif
 #pragma unroll
     for (int i = 0; i < NRT; ++i) {
-#if defined(NERF_WG_AHEAD2)
-      if (i + 2 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS reads (tile i+2)
-#elif !defined(NERF_WG_FRAG_JIT)
+#ifndef NERF_WG_FRAG_JIT
       if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS reads (tile i+1)
 #else
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads
@@ -2220,22 +2201,11 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     split3_bf16(ra[SET], fa[0], fa[1], fa[2]);
     load(set_c, st + 2);
     __builtin_amdgcn_sched_barrier(0);
-#ifdef NERF_K64_FRAG_AHEAD   // A/B: both column tiles' fragments up front, tile 1's reads overlapping tile 0's MFMAs
-    bf16x8 fxs[2][3];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) fxs[t][q] = *reinterpret_cast<const bf16x8*>(&Xs[buf][q][32 * t + c][8 * h]);
-#endif
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-#ifdef NERF_K64_FRAG_AHEAD
-      const bf16x8 (&fx)[3] = fxs[t];
-#else
       bf16x8 fx[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) fx[q] = *reinterpret_cast<const bf16x8*>(&Xs[buf][q][32 * t + c][8 * h]);
-#endif
       f32x16 v = acc[t];
       v = mfma_bf16(fa[0], fx[2], v);
       v = mfma_bf16(fa[1], fx[1], v);
