@@ -45,6 +45,9 @@ MFMA_F32_PEAK_TFLOPS = 157.3
 FLOP_FWD = 1_048_832
 FLOP_DGRAD = 2 * (7 * 256 * 256 + 256 * 128)                                   # 983,040
 FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 128 + 129 * 3)
+# the weight gradients' MFMA arithmetic under f16x3: bf16x6 (six bf16 products per fp32 product,
+# 2516.8/6 = 419.5 TFLOP/s); the vendor's sustained bf16 GEMM 1,377.1 TFLOP/s over the same count
+WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "bf16x6", 6, 1377.1 / 6
 
 
 def parse():
@@ -129,41 +132,30 @@ def dry_run(args, world, rank):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ok = ok and bool(torch.allclose(grad, torch.full((n,), (world + 1) / 2.0)))
-    ranks = [rank]
+    got = [(rank, 1e3 * elapsed / args.steps)]
     if group is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-        ranks = [None] * world
-        dist.all_gather_object(ranks, rank)
+        got = [None] * world
+        dist.all_gather_object(got, (rank, 1e3 * elapsed / args.steps))
+    ranks, rank_ms = [g[0] for g in got], [g[1] for g in got]
+    elapsed = max(rank_ms) * args.steps * 1e-3
     if rank == 0:
         print(json.dumps({"metric": "training steps/sec (dry run: gradient all-reduce only, gloo)",
                           "value": args.steps / elapsed, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
                           "higher_is_better": True, "scaling": "weak", "dry_run": True, "ranks": ranks,
-                          "allreduce_ok": ok, "config": {"parallelism": f"dp{world} (gloo all-reduce)"}}), flush=True)
+                          "rank_ms": rank_ms, "allreduce_ok": ok, "config": {"parallelism": f"dp{world} (gloo all-reduce)"}}), flush=True)
     if group is not None:
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    from nerfmi import launch
-    rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
-    if rc is not None:
-        sys.exit(rc)
-    if args.dry_run:
-        return dry_run(args, int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
-    # under a launcher (WORLD_SIZE set, 1 included) the RCCL group exists: broadcast, gradient
-    # all-reduce, barriers and the max-over-ranks timing all run on the device
-    world, rank, local, group = launch.init_ranks("nccl")
-    if group is None:
-        torch.cuda.set_device(local)
-    ranks = launch.rank_list(group)
+def measure(args, world, rank, group, ranks):
+    """Time args.steps training steps on this rank (args: steps, warmup, batch, arith,
+    no_cpu_baseline, cpu_seconds); every rank calls it, rank 0 gets the result dict (else None).
+    bench.py calls it for its "train" leg in the same process as the render bench."""
     import nerfmi
-    from nerfmi import _lib
     from nerfmi.dataset import SyntheticNeRFDataset
     from nerfmi.train import Trainer
+    prev_arith = nerfmi.get_mlp_arith()
     nerfmi.set_mlp_arith(args.arith)
     cfg = nerfmi.Config()
     np.random.seed(100 + rank)                    # each rank draws its own images / pixels
@@ -171,11 +163,10 @@ def main():
     batches = [ds.get_rays(batch_size=args.batch) for _ in range(args.warmup + args.steps)]
     torch.manual_seed(0)
     tr = Trainer(cfg, appearance_embeddings=ds.appearance_embeddings, group=group)
-    lib, P = _lib.load(), _lib.ptr
     stream = torch.cuda.current_stream()
 
     # stage timing: events around each stage on the launch stream
-    ev = {k: [] for k in ("fwd", "bwd", "allreduce", "adam")}
+    pending = []
 
     def step(b, timed):
         marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
@@ -191,10 +182,11 @@ def main():
         tr.optimizer_step()
         if timed:
             marks[4].record(stream)
-            ev["_pending"] = ev.get("_pending", []) + [marks]
+            pending.append(marks)
 
     for i in range(args.warmup):
         step(batches[i], False)
+    torch.cuda.synchronize()
     if group is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -205,12 +197,10 @@ def main():
     if group is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if group is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    rank_ms = gather_rank_ms(1e3 * elapsed / args.steps, group)
+    elapsed = max(rank_ms) * args.steps * 1e-3
     stage = {"fwd": [], "bwd": [], "allreduce": [], "adam": []}
-    for m in ev.get("_pending", []):
+    for m in pending:
         stage["fwd"].append(m[0].elapsed_time(m[1]))
         stage["bwd"].append(m[1].elapsed_time(m[2]))
         stage["allreduce"].append(m[2].elapsed_time(m[3]))
@@ -219,6 +209,7 @@ def main():
     # kernel-level timing of one extra (untimed) step: forward, data-gradient and weight-gradient phases
     kt = tr.profile_step(batches[-1]["rays_o"], batches[-1]["rays_d"], batches[-1]["rgb"],
                          batches[-1]["appearance_idx"])
+    out = None
     if rank == 0:
         M = args.batch * cfg.num_samples
         rays = args.batch * args.steps * world
@@ -226,8 +217,8 @@ def main():
                 "wgrad": (FLOP_WGRAD, kt["param_grads_ms"])}
         peaks = {"mlp_forward_train": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
                  "mlp_backward": MFMA_F32_PEAK_TFLOPS * (16 / 3 if args.arith == "f16x3" else 1),
-                 "wgrad": MFMA_F32_PEAK_TFLOPS * (16 / 6 if args.arith == "f16x3" else 1)}
-        vendor = ({"mlp_forward_train": 1323.5 / 3, "mlp_backward": 1323.5 / 3, "wgrad": 1377.1 / 6}
+                 "wgrad": MFMA_F32_PEAK_TFLOPS * (16 / WGRAD_PRODUCTS if args.arith == "f16x3" else 1)}
+        vendor = ({"mlp_forward_train": 1323.5 / 3, "mlp_backward": 1323.5 / 3, "wgrad": WGRAD_VENDOR}
                   if args.arith == "f16x3" else None)
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]
@@ -235,15 +226,18 @@ def main():
         traffic = pmc_traffic() if args.arith == "f16x3" else {}
         out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
                "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "ranks": ranks,
+               "rank_ms": rank_ms,
                "process_group": "nccl (RCCL)" if group is not None else None, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None,
-               "dtype": "fp32 (f16x3 split forward/data gradients, bf16x6 split weight gradients)"
+               "dtype": f"fp32 (f16x3 split forward/data gradients, {WGRAD_ARITH} split weight gradients)"
                         if args.arith == "f16x3" else "fp32",
                "data": "synthetic: teacher-rendered 800x800 scene (SyntheticNeRFDataset, 100 poses), batches "
                        "pre-generated in HBM; student = torch.manual_seed(0); NeRF(Config())",
                "config": {"workload": "chair-style training loop, one image per batch", "rays_per_gpu_per_step":
-                          args.batch, "n_samples": cfg.num_samples, "parallelism": f"dp{world} (RCCL all-reduce)"},
+                          args.batch, "n_samples": cfg.num_samples,
+                          "parallelism": f"dp{world} (RCCL all-reduce)" if group is not None
+                          else "dp1 (no process group, no collective)"},
                "mlp_arith_forward": args.arith,
                "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": peaks[dominant],
                             "unit": "TFLOP/s", "frac": ach / peaks[dominant],
@@ -254,6 +248,7 @@ def main():
                             "kernels_ms": {k: v[1] for k, v in kern.items()},
                             "kernels_tflops": {k: M * v[0] / (v[1] * 1e-3) / 1e12 for k, v in kern.items()},
                             "kernels_frac": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / peaks[k] for k, v in kern.items()},
+                            "kernels_peak": peaks,
                             # hipBLASLt's own sustained dense GEMM on this part (profiles/r02_gemm_f16_ceiling.log):
                             # f16 1,323.5 and bf16 1,377.1 TFLOP/s, divided by the split's product count
                             "kernels_frac_of_vendor_gemm": {k: M * v[0] / (v[1] * 1e-3) / 1e12 / vendor[k]
@@ -261,6 +256,38 @@ def main():
                "stage_ms": stage_ms, "phase_ms": kt}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    nerfmi.set_mlp_arith(prev_arith)
+    del tr, ds, batches
+    return out
+
+
+def gather_rank_ms(ms, group):
+    """Every rank's ms per step (rank order); [ms] without a process group."""
+    if group is None:
+        return [ms]
+    t = torch.tensor([ms], dtype=torch.float64, device="cuda")
+    got = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(got, t, group=group)
+    return [float(g.item()) for g in got]
+
+
+def main():
+    args = parse()
+    from nerfmi import launch
+    rc = launch.world_or_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:], check_devices=not args.dry_run)
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_run:
+        alone = not launch.under_launcher()
+        return dry_run(args, 1 if alone else int(os.environ["WORLD_SIZE"]), 0 if alone else int(os.environ.get("RANK", "0")))
+    # under a launcher (WORLD_SIZE set, 1 included) the RCCL group exists: broadcast, gradient
+    # all-reduce, barriers and the max-over-ranks timing all run on the device
+    world, rank, local, group = launch.init_ranks("nccl")
+    if group is None:
+        torch.cuda.set_device(local)
+    ranks = launch.rank_list(group)
+    out = measure(args, world, rank, group, ranks)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:
         dist.destroy_process_group()

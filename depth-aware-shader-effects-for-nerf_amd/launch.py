@@ -18,11 +18,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def under_launcher():
+    """True when a launcher started this process: WORLD_SIZE plus a rendezvous marker
+    (torch.distributed.run's TORCHELASTIC_RUN_ID, or MASTER_ADDR and MASTER_PORT).  A WORLD_SIZE left
+    over in the environment without one (a scheduler export, a parent shell) does not count: the
+    process runs alone instead of waiting on an env:// rendezvous nobody serves."""
+    if os.environ.get("WORLD_SIZE") is None:
+        return False
+    if os.environ.get("TORCHELASTIC_RUN_ID") or (os.environ.get("MASTER_ADDR") and os.environ.get("MASTER_PORT")):
+        return True
+    sys.stderr.write("nerfmi.launch: WORLD_SIZE is set but no launcher marker (TORCHELASTIC_RUN_ID or "
+                     "MASTER_ADDR/MASTER_PORT) is: running as a single process without a process group\n")
+    return False
+
+
 def world_or_launch(gpus, script, argv, check_devices=True):
     """Return None when this process is a rank that should run (WORLD_SIZE == gpus, or a 1-GPU run),
     or an exit status: the launched ranks' status, or 2 when --gpus contradicts WORLD_SIZE or the
     node has fewer GPUs than asked for."""
-    env_world = os.environ.get("WORLD_SIZE")
+    env_world = os.environ.get("WORLD_SIZE") if under_launcher() else None
     if env_world is not None:
         if int(env_world) != gpus:
             sys.stderr.write(f"{os.path.basename(script)}: --gpus {gpus} but WORLD_SIZE={env_world}: "
@@ -44,13 +58,13 @@ def world_or_launch(gpus, script, argv, check_devices=True):
 
 
 def init_ranks(backend="nccl"):
-    """(world, rank, local_rank, group) of this process.  Under a launcher (WORLD_SIZE set, world 1
+    """(world, rank, local_rank, group) of this process.  Under a launcher (`under_launcher()`, world 1
     included) the device is set to LOCAL_RANK and the process group is initialised on `backend`
     ("nccl" = RCCL over xGMI on ROCm), so the collectives of the benches and the CLI run on the
     device even on one GPU; a plain `python bench.py` has no group (None) and runs no collective."""
     import torch
     import torch.distributed as dist
-    if os.environ.get("WORLD_SIZE") is None:
+    if not under_launcher():
         return 1, 0, 0, None
     world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
