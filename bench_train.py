@@ -22,8 +22,9 @@ gradients 983,040; weight gradients 1,066,752 including bias columns — DESIGN.
 over their event-timed durations.  The forward runs on the MLP arithmetic selected by --arith
 (f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
 157.3).  Under f16x3 the data gradients run on split-f16 MFMA too (838.9) and the weight
-gradients on bf16x6 MFMA (six bf16 products per fp32 product: 2516.8/6 = 419.5 TFLOP/s); under
-f32 both run on fp32 MFMA (157.3).
+gradients on block-scaled split-f16 MFMA (three f16 products per fp32 product at per-chunk
+power-of-two scales, 838.9; NERFMI_WGRAD=bf16x6: six bf16 products, 419.5); under f32 both run on
+fp32 MFMA (157.3).
 cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on a 1024-ray
 batch on this host's cores.
 """
@@ -45,9 +46,15 @@ MFMA_F32_PEAK_TFLOPS = 157.3
 FLOP_FWD = 1_048_832
 FLOP_DGRAD = 2 * (7 * 256 * 256 + 256 * 128)                                   # 983,040
 FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 128 + 129 * 3)
-# the weight gradients' MFMA arithmetic under f16x3: bf16x6 (six bf16 products per fp32 product,
-# 2516.8/6 = 419.5 TFLOP/s); the vendor's sustained bf16 GEMM 1,377.1 TFLOP/s over the same count
-WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "bf16x6", 6, 1377.1 / 6
+# the weight gradients' MFMA arithmetic under f16x3: the 256-column GEMMs (7 of the 8 big ones and
+# dir/sigma) on split-f16 with per-chunk power-of-two scales (three f16 products per fp32 product:
+# 2516.8/3 = 838.9 TFLOP/s; vendor f16 GEMM 1,323.5 / 3); NERFMI_WGRAD=bf16x6 restores the bf16x6
+# GEMMs (six bf16 products: 2516.8/6 = 419.5 TFLOP/s; vendor bf16 1,377.1 / 6).  The layer-0 and
+# skip-PE GEMMs (K = 63) stay bf16x6 either way.
+if os.environ.get("NERFMI_WGRAD") == "bf16x6":
+    WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "bf16x6", 6, 1377.1 / 6
+else:
+    WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "block-scaled f16x3", 3, 1323.5 / 3
 
 
 def parse():

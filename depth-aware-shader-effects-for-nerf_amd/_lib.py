@@ -78,6 +78,7 @@ _SIGNATURES = {
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     "nerf_render_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int, ctypes.c_int]),
+    "nerf_render_chunk_rays": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
     "nerf_render_rays": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                         ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -123,7 +124,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 

@@ -4,6 +4,7 @@
 // stream order.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -238,7 +239,7 @@ using namespace nerf;
 extern "C" {
 
 const char* nerf_last_error(void) { return g_err; }
-int nerf_abi_version(void) { return 10; }
+int nerf_abi_version(void) { return 11; }
 
 int nerf_get_rays(int H, int W, float focal, const float* c2w_host, int row0, int nrows, float* rays_o,
                   float* rays_d, nerf_stream_t stream) {
@@ -396,6 +397,27 @@ int nerf_profile_mlp_end(float* ms, int64_t* samples, int capacity, int* count) 
   return NERF_OK;
 }
 
+// Launch-size limit.  A sample-parallel launch spans 2 threads per sample (the MLP: 256 per 128
+// samples) and a grid holds < 2^32 work-items per dimension, so one launch takes at most
+// 2^30 samples; larger calls run in ray chunks of nerf_render_chunk_rays rays
+// (the reference's volume_render has no such limit, src/render.py:5-97; its callers chunk at
+// config.chunk, run.py:209-231).
+// NERFMI_MAX_LAUNCH_SAMPLES (read once; test hook, >= 4096) lowers the limit so the GPU tests can
+// check a chunked call against the one-launch call at small sizes (tests/test_gpu_parity.py).
+static int64_t max_launch_samples() {
+  static const int64_t v = [] {
+    const char* e = getenv("NERFMI_MAX_LAUNCH_SAMPLES");
+    const long long x = e ? atoll(e) : 0;
+    return x >= 4096 && x < ((int64_t)1 << 30) ? (int64_t)x : ((int64_t)1 << 30);
+  }();
+  return v;
+}
+
+int64_t nerf_render_chunk_rays(int N, int Nf) {
+  const int per = N > Nf ? N : Nf;
+  return per >= 1 ? max_launch_samples() / per : 0;
+}
+
 int nerf_mlp_forward(const float* packed, const float* origins, const float* dirs, const float* z_vals, int64_t R,
                      int N, const float* ray_feat, float* rgb, float* sigma, const int32_t* out_slot, int out_T,
                      nerf_stream_t stream) {
@@ -404,7 +426,16 @@ int nerf_mlp_forward(const float* packed, const float* origins, const float* dir
   REQUIRE(z_vals || N == 1, "nerf_mlp_forward: without z_vals the origins are the points and N must be 1");
   REQUIRE(R == 0 || (packed && origins && ray_feat && rgb && sigma && (!z_vals || dirs)),
           "nerf_mlp_forward: null pointer");
-  return profiled_mlp(packed, origins, dirs, z_vals, R, N, ray_feat, rgb, sigma, out_slot, out_T, (hipStream_t)stream);
+  const int64_t rc_rays = nerf_render_chunk_rays(N, 0);
+  for (int64_t r0 = 0; r0 < R; r0 += rc_rays) {            // (one chunk unless R N > 2^30)
+    const int64_t n = R - r0 < rc_rays ? R - r0 : rc_rays;
+    const int64_t orow = out_slot ? (int64_t)out_T : (int64_t)N;   // output rows per ray
+    if (int rc = profiled_mlp(packed, origins + 3 * r0, dirs ? dirs + 3 * r0 : nullptr, z_vals ? z_vals + r0 * N : nullptr,
+                              n, N, ray_feat + r0 * kRayFeat, rgb + 3 * r0 * orow, sigma + r0 * orow,
+                              out_slot ? out_slot + r0 * N : nullptr, out_T, (hipStream_t)stream))
+      return rc;
+  }
+  return NERF_OK;
 }
 
 int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, int64_t B, int N, float* rgb_map,
@@ -432,11 +463,22 @@ static size_t carve(int64_t B, int N, int Nf, size_t* off) {
   return at;
 }
 
+int64_t nerf_render_chunk_rays(int N, int Nf);
+
+// (one chunk's worth: the chunks of a call past the launch-size limit reuse it in stream order)
 size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf) {
   if (B < 0 || N < 1 || Nf < 0) return 0;
+  const int64_t chunk = nerf_render_chunk_rays(N, Nf);
   size_t off[W_COUNT];
-  return carve(B, N, Nf, off);
+  return carve(B < chunk ? B : chunk, N, Nf, off);
 }
+
+static int render_rays_chunk(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
+                             double far, int N, int Nf, const float* t_vals, const float* u_lin, int perturb,
+                             const float* t_rand, const float* u_rand, uint64_t seed, int64_t ray0, const float* app,
+                             int64_t app_rows, float* rgb_map, float* depth_map, float* weights_out, float* z_out,
+                             float* coarse_rgb, float* coarse_depth, void* workspace, size_t ws_bytes,
+                             nerf_stream_t stream);
 
 int nerf_render_rays(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
                      double far, int N, int Nf, const float* t_vals, const float* u_lin, int perturb,
@@ -445,6 +487,36 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
                      float* coarse_rgb, float* coarse_depth, void* workspace, size_t ws_bytes,
                      nerf_stream_t stream) {
   REQUIRE(B >= 0 && ray0 >= 0, "nerf_render_rays: B=%lld ray0=%lld", (long long)B, (long long)ray0);
+  if (N < 1 || N > 4096 || Nf < 0 || N + Nf > 4096 || (Nf > 0 && (N > 256 || Nf > 1024)))
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_render_rays: N=%d Nf=%d outside the supported range", N, Nf);
+  // calls past the launch-size limit run in ray chunks: every per-ray input and output advances by
+  // the chunk's first ray, the in-kernel draws stay keyed by the global ray index (ray0 + c0), and
+  // each chunk carves the caller's workspace for its own (smaller) B
+  REQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_render_rays: app_rows=%lld with B=%lld",
+          (long long)app_rows, (long long)B);
+  const int64_t chunk = nerf_render_chunk_rays(N, Nf);
+  const int64_t T = Nf > 0 ? (int64_t)N + Nf : (int64_t)N;   // weights_out / z_out columns
+  for (int64_t c0 = 0; c0 < B || (B == 0 && c0 == 0); c0 += chunk) {
+    const int64_t n = B - c0 < chunk ? B - c0 : chunk;
+    const bool per_ray_app = app_rows > 1;
+    if (int rc = render_rays_chunk(packed, rays_o + 3 * c0, rays_d + 3 * c0, n, near, far, N, Nf, t_vals, u_lin, perturb,
+                                   t_rand ? t_rand + c0 * N : nullptr, u_rand ? u_rand + c0 * Nf : nullptr, seed,
+                                   ray0 + c0, per_ray_app ? app + c0 * kAppDim : app, per_ray_app ? n : app_rows,
+                                   rgb_map + 3 * c0, depth_map + c0, weights_out ? weights_out + c0 * T : nullptr,
+                                   z_out ? z_out + c0 * T : nullptr, coarse_rgb ? coarse_rgb + 3 * c0 : nullptr,
+                                   coarse_depth ? coarse_depth + c0 : nullptr, workspace, ws_bytes, stream))
+      return rc;
+    if (B == 0) break;
+  }
+  return NERF_OK;
+}
+
+static int render_rays_chunk(const float* packed, const float* rays_o, const float* rays_d, int64_t B, double near,
+                             double far, int N, int Nf, const float* t_vals, const float* u_lin, int perturb,
+                             const float* t_rand, const float* u_rand, uint64_t seed, int64_t ray0, const float* app,
+                             int64_t app_rows, float* rgb_map, float* depth_map, float* weights_out, float* z_out,
+                             float* coarse_rgb, float* coarse_depth, void* workspace, size_t ws_bytes,
+                             nerf_stream_t stream) {
   if (N < 1 || N > 4096 || Nf < 0 || N + Nf > 4096 || (Nf > 0 && (N > 256 || Nf > 1024)))
     return set_error(NERF_ERR_UNSUPPORTED, "nerf_render_rays: N=%d Nf=%d outside the supported range", N, Nf);
   if (B == 0) return NERF_OK;

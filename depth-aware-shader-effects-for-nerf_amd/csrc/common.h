@@ -85,6 +85,27 @@ constexpr int kRowLoadAux = NERF_ROW_LOAD_AUX;
 
 __device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
 
+// Max over the wave of a non-negative v, uniform result: DPP within each 16-lane row (quad swaps,
+// half-row and row mirrors), then the four rows' values by readlane.  No LDS, no branch.
+__device__ __forceinline__ float wave_max_nn(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));   // quad [1,0,3,2]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));   // quad [2,3,0,1]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
+// The block exponent record of layout.h for a block maximum m >= 0: -(kBlockExpBias + e), m < 2^e.
+__device__ __forceinline__ float block_exp_record(float m) {
+  int e;
+  frexpf(m, &e);
+  return -(float)(kBlockExpBias + (m > 0.0f ? e : kBlockExpZero));
+}
+
 // Counter-based uniform in [0,1) (splitmix64 finaliser), used when the caller
 // passes no explicit uniforms; it is a device RNG for throughput runs only.
 __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t idx) {

@@ -222,6 +222,21 @@ NERF_HD constexpr int64_t tile_col(int c) { return (int64_t)(c / 8) * 256; }
 NERF_HD constexpr int64_t tile_off(int64_t m, int f, int R) {
   return (m / 32) * 32 * (int64_t)R + (int64_t)(f / 8) * 256 + (m % 32) * 8 + f % 8;
 }
+// Block exponents (the split arithmetic's weight gradient, train.hip wgrad_h16w_kernel).  The
+// f16x3 forward and data-gradient kernels record, for each 32-sample block and each 256-wide
+// weight-gradient operand, the exponent e of the block's largest |value| (max < 2^e; an all-zero
+// block e = kBlockExpZero), as the integer-valued float -(kBlockExpBias + e), in row padding:
+//   save rows: entry j (j < 8: h_j) in enc_x's pad slot (feature kSaveEncX + 63) of sample j;
+//   gradient rows: entry j (j < 7: dpre_{j+1}; j = 7: [dpre_dir | dsigma_pre]) in the first pad
+//   float after dsigma_pre (feature kGradSigma + 1) of sample j.
+// Every other writer leaves those slots 0 (the f32 forward's zero pad, the other backward kernels),
+// which reads as "absent": the GEMM then finds the chunk's maximum itself.
+constexpr int kMetaSaveF = kSaveEncX + 63;
+constexpr int kMetaGradF = kGradSigma + 1;
+constexpr int kBlockExpBias = 1000;
+constexpr int kBlockExpZero = -126;
+NERF_HD constexpr bool block_exp_valid(float v) { return v <= -500.0f; }
+
 static_assert(kSaveRow % 8 == 0 && kGradRow % 8 == 0 && kSaveEncX % 8 == 0 && kSaveEncD % 8 == 0 &&
                   kSaveRDir % 8 == 0 && kSaveHd % 8 == 0 && kGradSigma % 8 == 0 && kGradHd % 8 == 0 &&
                   kGradRgb % 8 == 0,

@@ -294,6 +294,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   f32x16 acc[8];
   float m = 0.0f, part = 0.0f;
+  float bexp = 0.0f;   // training: lane j < 8 gathers the block exponent record of h_j (layout.h)
   float inv_cur = cst[kS16InvW + 0] / s_cur;                // exact: powers of two
   float s_nxt = pow2_scale(cst[kS16R + 0] * m_pe + cst[kS16B + 0]);
   STAMP16(1);
@@ -392,6 +393,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     }
     // the inputs of layer L are all known: the scale of layer L+1's inputs from the bound on y_L
     m = sample_max(m);
+    if constexpr (SAVE) {   // m = the sample's max of h_{L-1}: the wave's block exponent (uniform)
+      const float rec = block_exp_record(wave_max_nn(m));
+      bexp = (lane & 31) == L - 1 ? rec : bexp;
+    }
     float bound = cst[kS16R + L] * (L == kSkipLayer ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
     if (L + 1 == kSkipLayer) bound = fmaxf(bound, m_pe);    // layer 4 splits the PE at the same scale
     s_nxt = pow2_scale(bound);
@@ -442,6 +447,10 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   run_group<0, 8, 0, 0, kSidePrev, SAVE>(stream, s16_chunk0(8), lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
                         [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_prev(i, kk, ph, Sigma{}); });
   STAMP16(10);
+  if constexpr (SAVE) {     // h_7 (m: y_7 tiles 0-3 from layer 7's group B, tiles 4-7 from the colour layer's)
+    const float rec = block_exp_record(wave_max_nn(sample_max(m)));
+    bexp = (lane & 31) == 7 ? rec : bexp;
+  }
 
   // density head: sigma = ReLU(density_head(ReLU(h7))) (models.py:137-138), f32.
   const float sig = fmaxf(part + __shfl_xor(part, 32) + ws[kHidden], 0.0f);
@@ -501,12 +510,14 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
     out[c] = 1.0f / (1.0f + expf_rn(-v));                           // sigmoid (models.py:159-160)
   }
   if constexpr (SAVE) {
-    if (valid) {   // enc_x in the reference order (pe_feature; slot 63 is the zero pad), enc_d
+    if (valid) {   // enc_x in the reference order (pe_feature; slot 63: the block exponents, layout.h), enc_d
+      const float pad = (lane & 31) < 8 ? bexp : 0.0f;
 #pragma unroll
       for (int p = 0; p < kPeSteps; ++p) {
         const int f = pe_feature(p, h);
         const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? 0.0f : pe_mine[p * 64 + lane]), wrows,
+        static_assert(kSaveEncX + kPosEnc == kMetaSaveF, "enc_x's pad slot holds the block exponents");
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? pad : pe_mine[p * 64 + lane]), wrows,
                                               (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
       }
       const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);

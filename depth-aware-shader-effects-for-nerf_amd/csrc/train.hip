@@ -507,6 +507,7 @@ mlp_backward_kernel(const float* __restrict__ packed, const float* __restrict__ 
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
     grow[tile_col(kGradSigma)] = dsp;
+    grow[tile_col(kMetaGradF) + kMetaGradF % 8] = 0.0f;   // no block exponent (layout.h)
 #pragma unroll
     for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
@@ -719,6 +720,7 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
     grow[tile_col(kGradSigma)] = dsp;
+    grow[tile_col(kMetaGradF) + kMetaGradF % 8] = 0.0f;   // no block exponent (layout.h)
 #pragma unroll
     for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
@@ -909,6 +911,7 @@ mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restr
   const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
   if (valid && h == 0) {
     grow[tile_col(kGradSigma)] = dsp;
+    grow[tile_col(kMetaGradF) + kMetaGradF % 8] = 0.0f;   // no block exponent (layout.h)
 #pragma unroll
     for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
   }
@@ -1138,6 +1141,12 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
       }
   }
   m_dir = sample_max(m_dir);
+  // block exponent records (layout.h): lane j < 8 gathers entry j; [dpre_dir | dsigma_pre] is entry 7
+  float bexp = 0.0f;
+  {
+    const float rec = block_exp_record(wave_max_nn(fmaxf(m_dir, fabsf(dsp))));
+    bexp = (lane & 31) == 7 ? rec : bexp;
+  }
   // Every split scale carries the sample's sign sgn (odd samples negative).  The MFMA unit's f32
   // accumulation of f16 products is not correctly rounded and its error leans negative (-0.12 ulp
   // on average, profiles/r04/mfma_f16_accumulation_rounding.log); a gradient row of an odd sample is
@@ -1233,6 +1242,10 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
                                            });
     // the inputs of this layer are complete: the scale of d pre_{l-1} from the bound
     m = sample_max(m);
+    {   // m = the sample's max |d pre_l|: entry l - 1 (uniform over the wave)
+      const float rec = block_exp_record(wave_max_nn(m));
+      bexp = (lane & 31) == l - 1 ? rec : bexp;
+    }
     s_nxt = sgn * pow2_scale(cst[kT16C + l - 1] * m);
     m = 0.0f;
     if constexpr (last) {
@@ -1261,6 +1274,10 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
     bw_quarter<0, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
     bw_quarter<1, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
   });
+  // the records: sample j's feature kMetaGradF (lane half 1 writes a 0 four pad floats on; tail lanes'
+  // offsets lie outside the buffer range)
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h == 0 && (lane & 31) < 8 ? bexp : 0.0f), ga.rows,
+                                        (int)ga.loff + 4 * (int)(tile_col(kMetaGradF) + kMetaGradF % 8), 0, 0);
 }
 
 int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
@@ -1294,7 +1311,7 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
 // partial[c][n*KP + k'] = sum over samples m of chunk c of a[m][n] * x'[m][k'], k' < KP = K + 1,
 // where x'[m][k] = x[xrow(m)][k] for k < K and x'[m][K] = 1 (the bias column).  xrow(m) = m / x_div
 // (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).  Each chunk's
-// partial occupies wgrad_stride(N, K) floats (N*KP rounded up to 4, for 16-byte reduce loads).
+// partial occupies wgrad_stride(N, K) floats (N*KP rounded up to 4, for 16-byte reduce loads, + 4).
 constexpr int kWChunk = 2048;   // samples per chunk
 // Chunk length of a (N, K) weight gradient on the bf16x6 path: short enough that a 2^18-sample
 // step puts a block in every resident slot.  The 256x64-tile launches (K <= 64, N > 64: layer 0
@@ -1303,8 +1320,25 @@ constexpr int kWChunk = 2048;   // samples per chunk
 // than 3 tiles (the sigma and rgb heads) take 1024 / 512-sample chunks.
 // (N = 160: dir_linear's 128 rows + the density head's, the tile-major training path only)
 static inline bool wgrad_whole_tile(int N, int K) { return (N == 256 || N == 160) && K == 256; }
+// Whole-tile chunks of 2,048 samples (128 per 262K-sample step, half the CUs): on split-f16 the
+// launches are bound by HBM, not MFMA, and halving the chunk partials (~0.5 GB per step written and
+// read back) paid +1.7 % on the training step against 1,024-sample chunks (same-box A/B,
+// profiles/r05/ab_head3_pe_clen2k.log; under bf16x6 the 2,048-sample chunks had been 3.5 % slower).
+#ifndef NERF_WG_WHOLE_CLEN   // (A/B builds: the whole-tile chunk length and minimum chunk count)
+#define NERF_WG_WHOLE_CLEN kWChunk
+#endif
+#ifndef NERF_WG_MIN_CHUNKS
+#define NERF_WG_MIN_CHUNKS 128
+#endif
+#ifndef NERF_K64_CLEN   // (A/B builds: the 512 x 63 pair's chunk length and minimum chunk count)
+#define NERF_K64_CLEN (kWChunk / 2)
+#endif
+#ifndef NERF_K64_MIN_CHUNKS
+#define NERF_K64_MIN_CHUNKS 256
+#endif
 static inline int wgrad_chunk_len_big(int N, int K) {
-  if (wgrad_whole_tile(N, K)) return kWChunk / 2;   // wgrad_bf256_kernel: one block per chunk, 256 per step
+  if (wgrad_whole_tile(N, K)) return NERF_WG_WHOLE_CLEN;   // one block per chunk, 256 per step
+  if (K <= 64 && N == 2 * kHidden) return NERF_K64_CLEN;   // (the layer-0 / skip-PE pair)
   if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
                                                     // 3 % faster but doubled the reduction)
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
@@ -1314,11 +1348,13 @@ static inline int wgrad_chunk_len_big(int N, int K) {
 // there are >= 256 chunks: 4,096 rays in 1,024-row chunks ran 8 blocks, 80-100 us per launch.
 static inline int wgrad_chunk_len(int N, int K, int64_t M) {
   int c = wgrad_chunk_len_big(N, K);
-  while (c > 16 && (M + c - 1) / c < 256) c /= 2;
+  const int min_chunks = wgrad_whole_tile(N, K) ? NERF_WG_MIN_CHUNKS : (K <= 64 && N == 2 * kHidden) ? NERF_K64_MIN_CHUNKS : 256;
+  while (c > 16 && (M + c - 1) / c < min_chunks) c /= 2;
   return c;
 }
 
-NERF_HD inline int64_t wgrad_stride(int N, int K) { return (((int64_t)N * (K + 1)) + 3) & ~(int64_t)3; }
+// (+ 4 trailing floats: the split-f16 kernel's chunk exponent, wgrad_h16w_kernel)
+NERF_HD inline int64_t wgrad_stride(int N, int K) { return ((((int64_t)N * (K + 1)) + 3) & ~(int64_t)3) + 4; }
 
 // Fallback (unaligned operands): one wave per 32 (n) x 64 (k') tile of one chunk, operands
 // loaded straight from global memory (A = a^T fragment: n = l&31, sample = l>>5; B = x'
@@ -2115,6 +2151,245 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a once
 }
 
+// ------------------------------------------------- split-f16 ("f16x3") weight gradient, 256 columns
+// The whole-tile GEMM of wgrad_bf256w_kernel on v_mfma_f32_32x32x16_f16 with three products per
+// fp32 product instead of bf16x6's six: every operand value is split as v s = hi + lo (f16 each, lo =
+// f16(v s - hi), the residual exact in f32) and a k-step accumulates lo(a)hi(x) + hi(a)lo(x) +
+// hi(a)hi(x) (small terms first; the dropped lo lo term and the split residual are O(2^-22) of the
+// product), half the MFMAs and two thirds of the split VALU of bf16x6.  f16 lacks f32's exponent
+// range, so each operand carries one power-of-two scale per chunk, s = 2^(14 - e) with e the
+// exponent of the chunk's largest |value| (every v s < 2^14: no f16 overflow).  The MFMAs accumulate
+// in place (AGPRs) at those scales and the partial is unscaled once at the store (exact: powers of
+// two).  A value far below its chunk's maximum keeps an absolute error <= 2^-25 / s = 2^-39 of that
+// maximum, far below an fp32 sum's rounding of the terms near it.
+// The chunk maxima come from the producers: the f16x3 forward and data-gradient kernels record each
+// 32-sample block's exponent per operand slice (layout.h, block exponents); the kernel takes the
+// largest over its chunk's blocks.  Without records (rows from another writer) it first reads the
+// chunk once to find them (workgroup-uniform branch before the GEMM).
+constexpr int kH16EMin = -100;        // scale floor exponent (an all-zero or tiny chunk)
+struct H16Meta {                      // where the block exponents of a and x are (nullable: absent)
+  const float* a = nullptr;           // record of block 0; block b at + b * a_stride
+  int64_t a_stride = 0;
+  const float* x = nullptr;
+  int64_t x_stride = 0;
+  int a_cols = 256;                   // a columns whose values count (the partial's kept rows)
+};
+
+// v s = hi + lo for 8 values at scale s (hi by v_cvt_pk_f16_f32, lo by split_lo_pair)
+__device__ __forceinline__ void split2_f16(const float (&v)[8], float s, h16x8& hi, h16x8& lo) {
+  typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float x0 = v[2 * p] * s, x1 = v[2 * p + 1] * s;
+    const h16x2 hi2 = {(_Float16)x0, (_Float16)x1};
+    const h16x2 lo2 = __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), x0, x1));
+    hi[2 * p] = hi2[0];
+    hi[2 * p + 1] = hi2[1];
+    lo[2 * p] = lo2[0];
+    lo[2 * p + 1] = lo2[1];
+  }
+}
+
+template <bool BLK, int NRT = 8>
+__global__ void __launch_bounds__(256, 1)
+wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
+                  int clen, H16Meta meta, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][2][kWT][kBfRow];   // [buffer][hi, lo][column][sample]
+  __shared__ float wmax[4][2];
+  const int chunk = blockIdx.x;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;   // wave wk: columns 64 wk ..
+  const int h = lane >> 5, c = lane & 31;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(tid) + tid % 8) : 4u * (uint32_t)tid;
+  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;
+  uint32_t xvo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int xc = 64 * wk + 32 * t + c;
+    xvo[t] = BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)xc;
+  }
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[4][16], rx[4][2][8];
+  double bacc = 0.0;
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux));
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+
+  // ---- the chunk's exponents: from the block records (lanes 0..31: one block each), else by a pass
+  // over the chunk (a: column tid of the loaded rows, only the 32 NRT the partial keeps; x: the
+  // wave's fragment columns)
+  int Ea, Ex;
+  {
+    const int64_t b0 = m0 / 32, nb = (m1 - 1) / 32 - b0 + 1;   // blocks of the chunk (<= 32)
+    float ra_rec = 0.0f, rx_rec = 0.0f, bad = 0.0f;             // 1000 + e of lane's block; 1: a record absent
+    if (lane < nb && meta.a && meta.x) {
+      const float va = meta.a[(b0 + lane) * meta.a_stride], vx = meta.x[(b0 + lane) * meta.x_stride];
+      bad = (block_exp_valid(va) && block_exp_valid(vx)) ? 0.0f : 1.0f;
+      ra_rec = -va;
+      rx_rec = -vx;
+    }
+    const bool have = meta.a && meta.x && wave_max_nn(bad) == 0.0f;   // uniform (every wave alike)
+    if (have) {
+      Ea = (int)wave_max_nn(ra_rec) - kBlockExpBias;
+      Ex = (int)wave_max_nn(rx_rec) - kBlockExpBias;
+    } else {
+      // over the chunk's whole 32-sample blocks (the records' span: a chunk shorter than a block gets
+      // the exponents the records would give it)
+      float ma = 0.0f, mx = 0.0f;
+      const int64_t f0 = b0 * 32, f1 = (b0 + nb) * 32 < M ? (b0 + nb) * 32 : M;
+      for (int64_t ms = f0; ms < f1; ms += kBfStage) {
+        const uint32_t left = (uint32_t)(f1 - ms);
+        const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
+            BLK ? (int)(32 * lda4 - (ms % 32) * 32) : (int)((left < kBfStage ? left : kBfStage) * lda4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
+            BLK ? (int)(32 * ldx4 - (ms % 32) * 32) : (int)((left < kBfStage ? left : kBfStage) * ldx4), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          ma = fmaxf(ma, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), 0))));
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            mx = fmaxf(mx, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), 0))));
+      }
+      ma = wave_max_nn(tid < meta.a_cols ? ma : 0.0f);
+      mx = wave_max_nn(mx);
+      wmax[wk][0] = ma;                // (every lane the same value)
+      wmax[wk][1] = mx;
+      __syncthreads();
+      ma = fmaxf(fmaxf(wmax[0][0], wmax[1][0]), fmaxf(wmax[2][0], wmax[3][0]));
+      mx = fmaxf(fmaxf(wmax[0][1], wmax[1][1]), fmaxf(wmax[2][1], wmax[3][1]));
+      Ea = (int)(-block_exp_record(ma)) - kBlockExpBias;
+      Ex = (int)(-block_exp_record(mx)) - kBlockExpBias;
+    }
+    Ea = __builtin_amdgcn_readfirstlane(Ea < kH16EMin ? kH16EMin : Ea);
+    Ex = __builtin_amdgcn_readfirstlane(Ex < kH16EMin ? kH16EMin : Ex);
+  }
+  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
+
+  h16x8 fx[2][2][2];                   // split x fragments of stages st (fx[st & 1]) and st+1: [t][hi, lo]
+  auto split_x = [&](auto set_c, auto fb_c) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value, FB = decltype(fb_c)::value;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) split2_f16(rx[SET][t], sx, fx[FB][t][0], fx[FB][t][1]);
+  };
+  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) bacc += (double)ra[SET][j];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ra[SET][8 * o + j];
+      h16x8 hi, lo;
+      split2_f16(v, sa, hi, lo);
+      *reinterpret_cast<h16x8*>(&As[buf][0][tid][8 * o]) = hi;
+      *reinterpret_cast<h16x8*>(&As[buf][1][tid][8 * o]) = lo;
+    }
+  };
+  f32x16 acc[NRT][2];
+#pragma unroll
+  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;
+  load(C0{}, 0);
+  load(C1{}, 1);
+  load(C2{}, 2);
+  split_x(C0{}, C0{});
+  split_a(C0{}, 0);
+  __syncthreads();
+  // iteration st (set st % 4, buffers st % 2): stage st+3's loads; stage st's MFMAs with stage st+1's
+  // splits in their shadow; barrier
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value, FB = SET & 1;
+    using Nxt = std::integral_constant<int, (SET + 1) & 3>;
+    using Ld = std::integral_constant<int, (SET + 3) & 3>;
+    using FBn = std::integral_constant<int, FB ^ 1>;
+    load(Ld{}, st + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    h16x8 fa[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fa[0][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][c][8 * h]);
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) {
+      if (i + 1 < NRT) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fa[(i + 1) & 1][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
+      }
+      const h16x8 (&f)[2] = fa[i & 1];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma16(f[1], fx[FB][j][0], t);
+        t = mfma16(f[0], fx[FB][j][1], t);
+        acc[i][j] = mfma16(f[0], fx[FB][j][0], t);
+      }
+    }
+    split_x(Nxt{}, FBn{});
+    split_a(Nxt{}, FB ^ 1);
+    // schedule: per row tile 2 fragment reads (the next tile's), then its 6 MFMAs each followed by
+    // VALU of the next stage's splits; the split's LDS writes last
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);         // tile 0's reads
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) {
+      if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS reads (tile i+1)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 3, 0);     // VALU
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x200, 4, 0);         // DS writes
+    __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 4) {
+    iteration(C0{}, st);
+    iteration(C1{}, st + 1);
+    iteration(C2{}, st + 2);
+    iteration(std::integral_constant<int, 3>{}, st + 3);
+  }
+  // the partial at the chunk's scales; its exponent eo (true = stored 2^eo) in the partial's trailing
+  // slot, applied by the reduction (a VALU unscale here would pull the accumulators out of the AGPRs)
+  constexpr int KP = kWT + 1;
+  const int64_t stride = wgrad_stride(32 * NRT, kWT);
+  float* out = partial + (size_t)chunk * stride;
+#pragma unroll
+  for (int i = 0; i < NRT; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = 64 * wk + 32 * j + c;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+    }
+  if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // (the bias column: unscaled)
+  if (tid == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;   // acc = sum (a 2^(14-Ea)) (x 2^(14-Ex))
+}
+
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2123,10 +2398,15 @@ wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __res
 // registers, so two workgroups share a CU and keep more loads in flight (1 KiB of a + 252 B of x
 // per sample).  Loads run two stages ahead, unconditionally.  75 us per 262K-sample launch against
 // 105 us on 256 x 64 tiles of wgrad_bf_kernel (scripts/wgrad_libs_trace.sh, K=63).
-template <bool BLK>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
-__global__ void __launch_bounds__(512)
+// NW = 16 (DUAL): two 256-row gradients over the same x in one launch, rows 256.. from a2 (layer 0's
+// d pre_0 and the skip layer's d pre_4, both over enc_x: x is read once, and 16 waves per workgroup
+// keep twice the loads in flight): 512 x K partials, each thread loading one x sample per stage.
+template <bool BLK, int NW = 8>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
+__global__ void __launch_bounds__(64 * NW)
 wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int K,
-                    int64_t M, int clen, float* __restrict__ partial) {
+                    int64_t M, int clen, float* __restrict__ partial, const float* __restrict__ a2 = nullptr) {
+  static_assert(NW == 8 || NW == 16, "one or two 256-row gradients");
+  constexpr int XS = 16 / NW;        // x samples per thread and stage
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][64][kBfRow];
   const int chunk = blockIdx.x;
   const int64_t m0 = (int64_t)chunk * clen;
@@ -2134,15 +2414,17 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const int ac = 32 * w + c;
+  if (NW == 16 && w >= 8) a = a2;    // (wave-uniform)
+  const int ac = 32 * (w & 7) + c;
   const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h) : (uint32_t)(8 * h) * lda4 + 4u * (uint32_t)ac;
   const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
-  // x loader: column tid % 64 (past K: an offset beyond any resource, reads 0), samples 2p, 2p+1
+  // x loader: column tid % 64 (past K: an offset beyond any resource, reads 0), samples XS p .. + XS-1
   const int xc = tid & 63, xp = tid >> 6;
-  const uint32_t xvo = xc < K ? (BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 16 * xp) : (uint32_t)(2 * xp) * ldx4 + 4u * (uint32_t)xc)
+  const uint32_t xvo = xc < K ? (BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 8 * XS * xp)
+                                     : (uint32_t)(XS * xp) * ldx4 + 4u * (uint32_t)xc)
                               : 0x80000000u;
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[2][8], rx[2][2];
+  float ra[2][8], rx[2][XS];
   double bacc = 0.0;                 // bias column in double: one rounding per chunk
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
@@ -2159,14 +2441,14 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     for (int j = 0; j < 8; ++j)
       ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux));
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < XS; ++j)
       rx[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, (int)(j * xs4), kRowLoadAux));
   };
   auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
-    __bf16 p[3][2];
+    __bf16 p[3][XS];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < XS; ++j) {
       const float v = rx[SET][j];
       const __bf16 h0 = (__bf16)v;
       const float r1 = v - (float)h0;
@@ -2177,8 +2459,12 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-      *reinterpret_cast<bf16x2*>(&Xs[buf][q][xc][2 * xp]) = bf16x2{p[q][0], p[q][1]};
+      if constexpr (XS == 2) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<bf16x2*>(&Xs[buf][q][xc][2 * xp]) = bf16x2{p[q][0], p[q][1]};
+      } else {
+        Xs[buf][q][xc][xp] = p[q][0];
+      }
     }
   };
   f32x16 acc[2] = {f32x16{}, f32x16{}};
@@ -2222,7 +2508,7 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
     iteration(S1{}, st + 1);
   }
   const int KP = K + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(kWT, K);
+  float* out = partial + (size_t)chunk * wgrad_stride(32 * NW, K);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int kk = 32 * t + c;
@@ -2234,6 +2520,80 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   // bias column: this lane summed column 32w + c over its 8 samples of every stage
   bacc += __shfl_xor(bacc, 32);
   if (h == 0) out[(size_t)(32 * w + c) * KP + K] = (float)bacc;
+}
+
+// The rgb head's weight gradient (rgb_linear: 3 rows over hd, K = 128) on tile-major rows: a
+// streaming kernel, not a GEMM tile (an MFMA tile would keep 3 of its 128 rows).  A workgroup owns a
+// chunk of 16 blocks (512 samples); wave w the feature groups 4w..4w+3 of hd.  Per block and group
+// a lane reads one float4 (the group's 32 samples x 8 features are 1 KiB contiguous: lane l holds
+// sample l/2, features 8g + 4(l&1)..+3) and the sample's d rgb_pre (3 floats), and accumulates the
+// 3 x 4 products in double; at the chunk's end the 32 lanes of each parity are summed (shuffles,
+// double) into the chunk's partial (N = 3, K = 128 layout of wgrad_reduce_kernel; the bias column
+// from wave 0).  Reads hd once at full lines: ~134 MB per 262K-sample step.
+constexpr int kHeadChunkBlocks = 16;   // (512 chunks per 262K-sample step: two workgroups per CU)
+__global__ void __launch_bounds__(256)
+wgrad_head3_kernel(const float* __restrict__ a, const float* __restrict__ x, int64_t M, float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nblk = (M + 31) / 32;
+  const int64_t b0 = (int64_t)blockIdx.x * kHeadChunkBlocks;
+  const int64_t b1 = b0 + kHeadChunkBlocks < nblk ? b0 + kHeadChunkBlocks : nblk;
+  const int j = lane >> 1, par = lane & 1;
+  double acc[4][3][4] = {};
+  double bacc[3] = {0.0, 0.0, 0.0};
+  // the block's rows: gradient rows at d rgb_pre's group, save rows at hd's first group; the next
+  // block's loads are issued before this block's products
+  auto load = [&](int64_t b, f32x4& dv, f32x4 (&v)[4]) __attribute__((always_inline)) {
+    const float* ab = a + b * 32 * kGradRow;
+    const float* xb = x + b * 32 * kSaveRow;
+    dv = *reinterpret_cast<const f32x4*>(ab + 8 * j);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = *reinterpret_cast<const f32x4*>(xb + (4 * w + g) * 256 + 4 * lane);
+  };
+  f32x4 dv_n, v_n[4];
+  if (b0 < b1) load(b0, dv_n, v_n);
+  for (int64_t b = b0; b < b1; ++b) {
+    const f32x4 dv = dv_n;
+    f32x4 v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = v_n[g];
+    if (b + 1 < b1) load(b + 1, dv_n, v_n);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double d = (double)dv[c];
+      bacc[c] += par == 0 ? d : 0.0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[g][c][e] = fma(d, (double)v[g][e], acc[g][c][e]);
+    }
+  }
+  // sum the 32 lanes of each parity (xor 2 .. 32 keeps the parity), in a fixed order
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int m = 2; m < 64; m <<= 1) acc[g][c][e] += __shfl_xor(acc[g][c][e], m);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int m = 2; m < 64; m <<= 1) bacc[c] += __shfl_xor(bacc[c], m);
+  constexpr int KP = kDirHidden + 1;
+  float* out = partial + (size_t)blockIdx.x * wgrad_stride(3, kDirHidden);
+  if (lane < 2) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[c * KP + 8 * (4 * w + g) + 4 * lane + e] = (float)acc[g][c][e];
+    if (w == 0 && lane == 0) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) out[c * KP + kDirHidden] = (float)bacc[c];
+    }
+  }
 }
 
 // x_blk: x tile-major (BLK and x_div == 1); under BLK a row-major x with x_div == 1 (the appearance
@@ -2274,7 +2634,7 @@ struct WgradSplit {                  // rows n0 <= n < n_end of a weight gradien
 constexpr int kRedParts = NERF_RED_PARTS;
 __global__ void __launch_bounds__(64 * kRedParts)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w, int ldo,
-                    float* __restrict__ out_b, int accumulate, WgradSplit split) {
+                    float* __restrict__ out_b, int accumulate, WgradSplit split, int scaled) {
   // the chunk partials are added in double and rounded once: a gradient entry is a sum over up to
   // 2^18 samples with heavy cancellation (random-sign upstream gradients), and an fp32 running sum of
   // its 256 chunk partials cost up to ~10x the fp32 CPU autograd's error on the bias columns
@@ -2292,7 +2652,7 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] += (double)v[e];
   };
-  if (col4 * 4 < stride) {
+  if (col4 * 4 < stride && !scaled) {
     const f32x4* p = reinterpret_cast<const f32x4*>(partial) + col4;
     const int64_t s4 = stride / 4;
     int c = c0;
@@ -2304,6 +2664,33 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
       for (int u = 0; u < 8; ++u) add(v[u]);
     }
     for (; c < c1; ++c) add(p[c * s4]);
+  } else if (col4 * 4 < stride) {
+    // split-f16 partials: chunk c's values times 2^(its exponent), the bias column as stored (exact in
+    // double: powers of two)
+    const f32x4* p = reinterpret_cast<const f32x4*>(partial) + col4;
+    const int* ex = reinterpret_cast<const int*>(partial) + stride - 4;
+    const int64_t s4 = stride / 4;
+    bool bias[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = (col4 * 4 + e) % (K + 1) == K;
+    auto add_scaled = [&](const f32x4& v, int x) __attribute__((always_inline)) {
+      const double sc = ldexp(1.0, x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += bias[e] ? (double)v[e] : (double)v[e] * sc;
+    };
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      f32x4 v[8];
+      int x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = p[(c + u) * s4];
+        x[u] = ex[(c + u) * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) add_scaled(v[u], x[u]);
+    }
+    for (; c < c1; ++c) add_scaled(p[c * s4], ex[c * stride]);
   }
   part[q][threadIdx.x & 63] = acc;
   __syncthreads();
@@ -2348,12 +2735,58 @@ static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, 
   return check_launch("wgrad_lds_kernel");
 }
 
+static int launch_wgrad_head3(const float* a, const float* x, int64_t M, float* out_w, float* out_b, float* ws,
+                              size_t ws_floats, hipStream_t s) {
+  if (M == 0) return NERF_OK;
+  const int chunks = (int)(((M + 31) / 32 + kHeadChunkBlocks - 1) / kHeadChunkBlocks);
+  if ((size_t)chunks * wgrad_stride(3, kDirHidden) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "wgrad_head3: workspace");
+  hipLaunchKernelGGL(wgrad_head3_kernel, dim3((unsigned)chunks), dim3(256), 0, s, a, x, M, ws);
+  if (int rc = check_launch("wgrad_head3_kernel")) return rc;
+  const int64_t cols4 = wgrad_stride(3, kDirHidden) / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks, 3,
+                     kDirHidden, out_w, kDirHidden, out_b, 0, WgradSplit{}, 0);
+  return check_launch("wgrad_reduce_kernel");
+}
+
+// Layer 0's weight gradient (d pre_0 over enc_x) and the skip layer's PE columns (d pre_4 over
+// enc_x) as one 512 x 63 GEMM over the tile-major rows (wgrad_bf_k64_kernel<NW = 16>): enc_x is read
+// once; rows 0..255 go to layer 0's weight + bias, rows 256.. to the skip weight's PE columns.
+static int launch_wgrad_pe_pair(const float* save, const float* grad, int64_t M, float* w0, float* b0, float* w4,
+                                float* ws, size_t ws_floats, hipStream_t s) {
+  if (M == 0) return NERF_OK;
+  const int clen = wgrad_chunk_len(2 * kHidden, kPosEnc, M);
+  const int chunks = (int)((M + clen - 1) / clen);
+  if ((size_t)chunks * wgrad_stride(2 * kHidden, kPosEnc) > ws_floats)
+    return set_error(NERF_ERR_WORKSPACE, "wgrad pe pair: workspace");
+  hipLaunchKernelGGL((wgrad_bf_k64_kernel<true, 16>), dim3((unsigned)chunks), dim3(1024), 0, s, grad + tile_col(0), kGradRow,
+                     save + tile_col(kSaveEncX), kSaveRow, kPosEnc, M, clen, ws, grad + tile_col(4 * kHidden));
+  if (int rc = check_launch("wgrad_bf_k64_kernel<16>")) return rc;
+  const WgradSplit skip{kHidden, w4 + kHidden, kHidden + kPosEnc, kPosEnc, nullptr};
+  const int64_t cols4 = wgrad_stride(2 * kHidden, kPosEnc) / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks,
+                     2 * kHidden, kPosEnc, w0, kPosEnc, b0, 0, skip, 0);
+  return check_launch("wgrad_reduce_kernel");
+}
+
+// The 256-column weight gradients of the split arithmetic run on split-f16 MFMA (wgrad_h16w_kernel)
+// unless NERFMI_WGRAD=bf16x6 is set (read once; the bf16x6 kernel is kept for same-process A/Bs).
+static bool wgrad_h16() {
+  static const bool on = [] {
+    const char* e = getenv("NERFMI_WGRAD");
+    return !(e && strcmp(e, "bf16x6") == 0);
+  }();
+  return on;
+}
+
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
 // appearance projection's x (the embedding rows, one per ray) is row-major: x_tiled = false.
+// meta: the block exponents of a and x (layout.h) for the split-f16 whole-tile kernel (nullable).
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
-                 const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true) {
+                 const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true,
+                 const H16Meta* meta = nullptr) {
+  const H16Meta hm = meta ? *meta : H16Meta{};
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
@@ -2362,14 +2795,28 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     return set_error(NERF_ERR_BAD_ARG, "wgrad: tile-major operands must be aligned with row lengths % 8 == 0");
   const bool x_blk = tiled && x_tiled && x_div == 1;   // x tile-major
   int rc;
+  bool scaled = false;                                  // partials of wgrad_h16w_kernel (chunk exponents)
   // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
+    const bool h16 = wgrad_h16();
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
-                         ws);
-      rc = check_launch("wgrad_bf256w_kernel<5>");
+      if (h16)
+        hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
+                           hm, ws);
+      else
+        hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
+                           ws);
+      rc = check_launch("wgrad whole-tile <5>");
+      scaled = h16;
+    } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
+      if (tiled)
+        hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
+      else
+        hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
+      rc = check_launch("wgrad_h16w_kernel");
+      scaled = true;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
 #if !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
       if (tiled)
@@ -2419,7 +2866,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   if (rc) return rc;
   const int64_t cols4 = wgrad_stride(N, K) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks, N, K,
-                     out_w, ldo, out_b, accumulate, split ? *split : WgradSplit{});
+                     out_w, ldo, out_b, accumulate, split ? *split : WgradSplit{}, (int)scaled);
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -2702,6 +3149,17 @@ static int pg_streams(PgStreams** out) {
   return NERF_OK;
 }
 
+// Where the block exponents of gradient entry ja and save entry jx live (layout.h)
+static H16Meta block_exps(const float* save, const float* grad, int ja, int jx) {
+  H16Meta m;
+  if (ja < 0 || jx < 0) return m;
+  m.a = grad + tile_col(kMetaGradF) + 8 * ja + kMetaGradF % 8;
+  m.a_stride = 32 * (int64_t)kGradRow;
+  m.x = save + tile_col(kMetaSaveF) + 8 * jx + kMetaSaveF % 8;
+  m.x_stride = 32 * (int64_t)kSaveRow;
+  return m;
+}
+
 // The jobs, on streams sa / sb with partial buffers wa / wb (wfl floats each) and the ray-sum
 // buffers at `rays` (N >= kRaySumMinN).
 static int param_grads_jobs(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
@@ -2713,26 +3171,43 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   // tiles (416 -> ~300 us per step).
   // save and grad are tile-major rows (layout.h): a slice starting at feature c is the same layout at
   // float offset tile_col(c).  Stream B: the K <= 64 GEMMs, layers 6-7 and the heads below.
-  struct Job { int a; int n; int x; int K; int p; int k0; int ldo; bool bias; bool b; };
+  // ja / jx: the block-exponent entries of a and x (layout.h; -1: none)
+  struct Job { int a; int n; int x; int K; int p; int k0; int ldo; bool bias; bool b; int ja; int jx; };
   constexpr int kSkipK = kHidden + kPosEnc;
   const Job jobs[] = {
-      {0, kHidden, kSaveEncX, kPosEnc, 0, 0, kPosEnc, true, true},
-      {1 * kHidden, kHidden, save_h(0), kHidden, 2, 0, kHidden, true, false},
-      {2 * kHidden, kHidden, save_h(1), kHidden, 4, 0, kHidden, true, false},
-      {3 * kHidden, kHidden, save_h(2), kHidden, 6, 0, kHidden, true, false},
-      {4 * kHidden, kHidden, save_h(3), kHidden, 8, 0, kSkipK, true, false},                  // h3 ..
-      {4 * kHidden, kHidden, save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false, true},  // .. | enc_x
-      {5 * kHidden, kHidden, save_h(4), kHidden, 10, 0, kHidden, true, false},
-      {6 * kHidden, kHidden, save_h(5), kHidden, 12, 0, kHidden, true, true},
-      {7 * kHidden, kHidden, save_h(6), kHidden, 14, 0, kHidden, true, true},
-      {kGradRgb, 3, kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true, false},
+      {0, kHidden, kSaveEncX, kPosEnc, 0, 0, kPosEnc, true, true, -1, -1},
+      {1 * kHidden, kHidden, save_h(0), kHidden, 2, 0, kHidden, true, false, 0, 0},
+      {2 * kHidden, kHidden, save_h(1), kHidden, 4, 0, kHidden, true, false, 1, 1},
+      {3 * kHidden, kHidden, save_h(2), kHidden, 6, 0, kHidden, true, false, 2, 2},
+      {4 * kHidden, kHidden, save_h(3), kHidden, 8, 0, kSkipK, true, false, 3, 3},                  // h3 ..
+      {4 * kHidden, kHidden, save_h(3) + kHidden, kPosEnc, 8, kHidden, kSkipK, false, true, -1, -1},  // .. | enc_x
+      {5 * kHidden, kHidden, save_h(4), kHidden, 10, 0, kHidden, true, false, 4, 4},
+      {6 * kHidden, kHidden, save_h(5), kHidden, 12, 0, kHidden, true, true, 5, 5},
+      {7 * kHidden, kHidden, save_h(6), kHidden, 14, 0, kHidden, true, true, 6, 6},
+      {kGradRgb, 3, kSaveHd, kDirHidden, P_RGB_W, 0, kDirHidden, true, false, -1, -1},
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
+#ifndef NERF_PE_SEPARATE   // (A/B build: layer 0 and the skip PE columns as two K = 63 launches)
+  if ((rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
+#endif
   for (const Job& j : jobs) {
+#ifndef NERF_PE_SEPARATE
+    if (j.K == kPosEnc) continue;            // (in the pair above)
+#endif
     if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
+#ifndef NERF_HEAD3_GEMM   // (A/B build: the rgb head on the 128 x 128 tile GEMM)
+    if (j.a == kGradRgb) {   // the rgb head: the streaming kernel (3 rows)
+      if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
+                                   j.b ? wb : wa, wfl, j.b ? sb : sa)))
+        return rc;
+      continue;
+    }
+#endif
+    const H16Meta hm = block_exps(save, grad, j.ja, j.jx);
     if ((rc = launch_wgrad(grad + tile_col(j.a), kGradRow, j.n, save + tile_col(j.x), kSaveRow, j.K, 1, M, g[j.p] + j.k0,
-                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? wb : wa, j.b ? sb : sa, nullptr, true)))
+                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? wb : wa, j.b ? sb : sa, nullptr, true, true,
+                           j.ja >= 0 ? &hm : nullptr)))
       return rc;
   }
   static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
@@ -2749,8 +3224,10 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     constexpr int kDirRows = 160;
     if (wgrad_workspace_floats(M, kDirRows, kWT) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
+    H16Meta hm = block_exps(save, grad, 7, 7);
+    hm.a_cols = kDirHidden + 1;                            // d pre_dir, d sigma (rows 129.. are dropped)
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
-                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true)))
+                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm)))
       return rc;
     hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, sb, grad, save, N, S, E);
     if ((rc = check_launch("ray_sums_kernel"))) return rc;

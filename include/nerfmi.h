@@ -46,7 +46,9 @@ const char* nerf_last_error(void);
  * and backward, include/nerfmi_train.h; 8: nerf_frame_fog; 9: nerf_render_rays' ray0 (in-kernel
  * draws keyed by the global ray index), nerf_train_forward's weights/z outputs,
  * nerf_composite_backward_grad; 10: tile-major save / gradient rows, NERF_TILE_ROWS, and the
- * two-stream nerf_param_grads with its larger workspace). */
+ * two-stream nerf_param_grads with its larger workspace; 11: nerf_render_chunk_rays (calls past
+ * the launch-size limit run in ray chunks), block exponent records in the save / gradient rows'
+ * padding, the split-f16 weight gradient). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays
@@ -180,6 +182,12 @@ int nerf_composite(const float* rgb, const float* sigma, const float* z_vals, in
  * nerf_rng_uniforms; 0 for a whole batch).  The workspace must hold
  * nerf_render_workspace_bytes(B, N, Nf) bytes. */
 size_t nerf_render_workspace_bytes(int64_t B, int N, int Nf);
+/* Rays per launch chunk: one launch spans at most 2^30 samples (the grid limit of the sample-
+ * parallel kernels), so nerf_render_rays (and nerf_mlp_forward, with Nf = 0) run a call of more
+ * than nerf_render_chunk_rays(N, Nf) rays as consecutive chunks of that many rays, bit-identical
+ * to one launch (the draws are keyed by the global ray index); nerf_render_workspace_bytes covers
+ * one chunk.  0 when N and Nf are both < 1. */
+int64_t nerf_render_chunk_rays(int N, int Nf);
 int nerf_render_rays(const float* packed, const float* rays_o, const float* rays_d, int64_t B,
                      double near, double far, int N, int Nf, const float* t_vals,
                      const float* u_lin, int perturb, const float* t_rand, const float* u_rand,

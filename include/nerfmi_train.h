@@ -32,6 +32,11 @@ extern "C" {
  * of sample m's row (row length R) is float (m/32)*32*R + (f/8)*256 + (m%32)*8 + f%8, and a buffer
  * of M samples holds NERF_TILE_ROWS(M) rows (the last block whole; its rows past M are zero). */
 #define NERF_TILE_ROWS(M) ((((M) + 31) / 32) * 32)
+/* Block exponents (ABI 11, f16x3 only): sample j of each 32-sample block carries, in enc_x's pad
+ * slot (save feature 1087) the exponent record of h_j (j < 8), and in the float after dsigma
+ * (gradient feature 2177) that of dpre_{j+1} (j < 7) or [dpre_dir | dsigma] (j = 7): -(1000 + e)
+ * with e = frexp's exponent of the block's largest |value| (-126 for an all-zero block); 0 = absent.
+ * nerf_param_grads' split-f16 weight gradient scales each chunk from them (csrc/layout.h). */
 /* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):
  * trunk layers 0..7 (256 bits each) and r_dir (128 bits), 272 bytes (csrc/layout.h kMaskRow). */
 #define NERF_MASK_ROW 68

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 10
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_bad_arguments_are_reported_not_launched():
@@ -44,6 +44,7 @@ def test_bad_arguments_are_reported_not_launched():
     assert rc == 1 and b"N must be 1" in lib.nerf_last_error()
     assert lib.nerf_render_workspace_bytes(0, 64, 128) == 0 or lib.nerf_render_workspace_bytes(0, 64, 128) >= 0
     assert lib.nerf_render_workspace_bytes(-1, 64, 0) == 0
+
     # empty inputs are a no-op, not an error
     assert lib.nerf_composite(None, None, None, 0, 64, None, None, None, None) == 0
     # training entry points
@@ -69,8 +70,8 @@ def test_bad_arguments_are_reported_not_launched():
     clen = 1024
     while clen > 16 and -(-5000 // clen) < 256:
         clen //= 2
-    assert clen == 16 and ws == -(-5000 // clen) * 256 * 257 * 4
-    assert lib.nerf_wgrad_workspace_bytes(262144, 256, 256) == 256 * 256 * 257 * 4   # production size: 1024-sample chunks
+    assert clen == 16 and ws == -(-5000 // clen) * (256 * 257 + 4) * 4
+    assert lib.nerf_wgrad_workspace_bytes(262144, 256, 256) == 256 * (256 * 257 + 4) * 4   # production size: 1024-sample chunks
     assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2312) * 4
     assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, None, 0, None, None) == 0
     # post effects
@@ -564,3 +565,23 @@ def test_host_abi_under_asan_ubsan():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "AddressSanitizer" not in out and "runtime error" not in out, out[-3000:]
+
+
+def test_render_chunk_plan():
+    """nerf_render_rays / nerf_mlp_forward run a call of more than 2^30 samples per launch (the
+    sample-parallel grids' limit) as ray chunks (capi.hip); the plan and the workspace are host
+    arithmetic, checked here without a launch."""
+    lib = _lib.load()
+    assert lib.nerf_render_chunk_rays(64, 128) == (1 << 30) // 128
+    assert lib.nerf_render_chunk_rays(64, 0) == (1 << 24)
+    assert lib.nerf_render_chunk_rays(256, 1024) == (1 << 20)
+    assert lib.nerf_render_chunk_rays(0, 0) == 0
+    # the workspace covers one chunk: a 2^25-ray H1 call (2^32 fine samples) needs no more than
+    # a 2^23-ray one, and an ordinary frame is unchanged
+    big = lib.nerf_render_workspace_bytes(1 << 25, 64, 128)
+    assert big == lib.nerf_render_workspace_bytes(1 << 23, 64, 128) > 0
+    assert lib.nerf_render_workspace_bytes(640_000, 64, 128) < big
+    # the appearance-row check runs before any chunk (app_rows must be 0, 1 or B)
+    rc = lib.nerf_render_rays(None, None, None, 10, 2.0, 6.0, 64, 128, None, None, 1, None, None, 0, 0, None, 5,
+                              None, None, None, None, None, None, None, 0, None)
+    assert rc == 1 and b"app_rows" in lib.nerf_last_error()

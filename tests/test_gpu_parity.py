@@ -9,6 +9,8 @@ Tolerances (north star: 1e-4 relative fp32 on rgb/depth, bit-exact ray indices):
     in torch's CPU order and the double prefix sums are exact); behind a GPU-computed coarse pass
     the weights already differ by ~1e-6 relative, so z there is held to 1e-5 relative.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -350,7 +352,7 @@ def test_hierarchical_extreme_sizes(nerfmi_mod, model, ref_state, app_vec, golde
     the GPU's merged z, as in test_full_frame_properties)."""
     o, d = crop(golden, "chair", 24)
     torch.manual_seed(14)
-    for N, Nf in ((256, 1024), (50, 70), (33, 1), (7, 200)):
+    for N, Nf in ((256, 1024), (50, 70), (33, 1), (7, 200), (64, 195)):   # (64, 195): T > 256, T % 4 != 0
         u = torch.rand(o.shape[0], Nf)
         rgb, depth, ex = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, N, Nf,
                                                 appearance_embedding=app_vec.cuda(), perturb=False,
@@ -365,6 +367,75 @@ def test_hierarchical_extreme_sizes(nerfmi_mod, model, ref_state, app_vec, golde
         r_fix, d_fix, _ = O._pass(ref_state, pts, dn, z, app_vec)
         close(rgb, r_fix, what=f"fine rgb, same z, N={N} Nf={Nf}")
         close(depth, d_fix, what=f"fine depth, same z, N={N} Nf={Nf}")
+
+
+def test_render_unaligned_outputs(nerfmi_mod, model, ref_state, app_vec, golden):
+    """nerf_render_rays with weights_out and z_out one float off 16-byte alignment (views into a larger
+    caller buffer): the merged fine composite takes its scalar-store variants (composite.hip) at
+    T = 192 (staged) and T = 259 (unstaged); maps, weights and merged z match the aligned call, and
+    the fine maps the oracle's fine pass on the same z."""
+    from nerfmi import _lib
+    from nerfmi.models import app_rows
+    from nerfmi.ray_utils import linspace_table
+    from nerfmi.render import packed_for
+    lib, dev = _lib.load(), _lib.device()
+    o, d = crop(golden, "chair", 24)
+    B = o.shape[0]
+    torch.manual_seed(15)
+    for N, Nf in ((64, 128), (64, 195)):
+        T = N + Nf
+        u = torch.rand(B, Nf)
+        rgb_a, depth_a, ex = nerfmi_mod.render_rays(model, o.cuda(), d.cuda(), 2.0, 6.0, N, Nf,
+                                                    appearance_embedding=app_vec.cuda(), perturb=False,
+                                                    hierarchical=True, u_rand=u)
+        oo, dd = o.reshape(-1, 3).cuda().contiguous(), d.reshape(-1, 3).cuda().contiguous()
+        app, rows = app_rows(app_vec, B, dev)
+        wbuf, zbuf = torch.zeros(B * T + 1, device=dev), torch.zeros(B * T + 1, device=dev)
+        w, z = wbuf[1:], zbuf[1:]                        # 4 bytes past a 16-byte boundary
+        assert w.data_ptr() % 16 != 0 and z.data_ptr() % 16 != 0
+        rgb, depth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
+        crgb, cdepth = torch.empty(B, 3, device=dev), torch.empty(B, device=dev)
+        ws = torch.empty(lib.nerf_render_workspace_bytes(B, N, Nf), dtype=torch.uint8, device=dev)
+        P = _lib.ptr
+        _lib.check(lib.nerf_render_rays(P(packed_for(model)), P(oo), P(dd), B, 2.0, 6.0, N, Nf, P(linspace_table(N, dev)),
+                                        P(linspace_table(Nf, dev, drop_last=True)), 0, None, P(u.cuda().contiguous()), 0,
+                                        0, P(app), rows, P(rgb), P(depth), P(w), P(z), P(crgb), P(cdepth), P(ws),
+                                        ws.numel(), _lib.stream()), "nerf_render_rays")
+        torch.cuda.synchronize()
+        close(rgb, rgb_a.reshape(B, 3), rtol=1e-6, what=f"rgb T={T}")
+        close(depth, depth_a.reshape(B), rtol=1e-6, what=f"depth T={T}")
+        close(w.reshape(B, T), ex["weights"].reshape(B, T), rtol=1e-6, what=f"weights T={T}")
+        assert torch.equal(z.reshape(B, T).cpu(), ex["z_vals"].cpu()), T
+        dn = O.normalize(d)
+        zc = z.reshape(B, T).cpu()
+        r_fix, d_fix, _ = O._pass(ref_state, o[:, None, :] + dn[:, None, :] * zc[..., None], dn, zc, app_vec)
+        close(rgb, r_fix, what=f"fine rgb vs oracle, same z, T={T}")
+        close(depth.reshape(B, 1), d_fix, what=f"fine depth vs oracle, same z, T={T}")
+
+
+def test_render_chunked_matches_one_launch(nerfmi_mod, tmp_path):
+    """A call past the launch-size limit runs as ray chunks (capi.hip, nerf_render_chunk_rays): with the
+    limit lowered to 2^16 samples in a child process (NERFMI_MAX_LAUNCH_SAMPLES), a 3,000-ray 64 + 128
+    H1 render with per-ray appearance rows, a ray offset and in-kernel draws runs as 6 chunks of 512
+    rays (nerf_render_rays) and as 3 + 6 chunk launches stage by stage (nerf_mlp_forward): every output
+    equals the one-launch render of this process bit for bit."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import render_chunked
+    ref = render_chunked.render()
+    out = tmp_path / "chunked.pt"
+    env = dict(os.environ, NERFMI_MAX_LAUNCH_SAMPLES=str(1 << 16))
+    from nerfmi import _lib
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "render_chunked.py"), str(out), _lib.get_mlp_arith()],
+                       env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert set(got) == set(ref)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
 
 
 def test_full_frame_properties(nerfmi_mod, model, ref_state, app_vec, golden_meta, arith):

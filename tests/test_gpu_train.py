@@ -96,6 +96,22 @@ def mostly_close(a, b, rtol=1e-3, frac=0.999):
     return ok.mean() >= frac, ok.mean()
 
 
+def block_records(rows, slices):
+    """The block exponent records (layout.h) rows should carry: entry j of 32-sample block b, in row
+    32 b + j, is -(1000 + e) for e = frexp's exponent of the block's largest |value| in slices[j]
+    (an all-zero block: e = -126); every other row 0."""
+    M = rows.shape[0]
+    out = np.zeros(M, np.float32)
+    for b in range(0, M, 32):
+        for j, sl in enumerate(slices):
+            if b + j >= M:
+                break
+            m = float(np.abs(rows[b:b + 32, sl]).max())
+            e = int(np.frexp(np.float32(m))[1]) if m > 0 else -126
+            out[b + j] = -(1000 + e)
+    return out
+
+
 def packed_of(state, dev):
     L = _lib()
     lib = L.load()
@@ -258,6 +274,7 @@ def _mlp_forward_backward(state, app, R=96, N=11, seed=3, draw=None):
         for l in range(9):
             sl = slice(256 * l, 256 * l + (256 if l < 8 else 128))
             assert rel_l2(g1[:, sl], g2[:, sl]) < 1e-5, (l, rel_l2(g1[:, sl], g2[:, sl]))
+        assert np.all(g2[:, 2177] == 0)   # the activation-mask kernel records no block exponents
         check_mask_words(L.untile(save.cpu(), M), masks.cpu())
     # oracle in float64 on the points the kernel evaluated (o + d z in fp32, render.py:22 / ray_utils.py:86)
     pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
@@ -287,22 +304,179 @@ def test_forward_saves_are_the_activations(ref_state, app_vec, with_app, N):
         assert rel_l2(save[:, off:off + 256], h) < 1e-5, l
     enc_x = O.positional_encoding(r["pts"], 10).numpy()
     np.testing.assert_allclose(save[:, 1024:1087], enc_x, rtol=1e-5, atol=2e-6)
-    assert np.all(save[:, 1087] == 0)
+    # enc_x's pad slot: the block exponent records of h_0..h_7 under f16x3 (layout.h), else the zero pad
+    if _lib().get_mlp_arith() == "f16x3":
+        exp = block_records(save, [slice(o, o + 256) for o in offs])
+        np.testing.assert_array_equal(save[:, 1087], exp)
+    else:
+        assert np.all(save[:, 1087] == 0)
     enc_d = O.positional_encoding(r["dexp"], 4).numpy()
     np.testing.assert_allclose(save[:, 2112:2139], enc_d, rtol=1e-5, atol=2e-6)
     assert np.all(save[:, 2139:2144] == 0)
 
 
+def test_gradient_block_records(ref_state, app_vec):
+    """The f16x3 data-gradient kernel records each block's exponent of d pre_1..7 and [d pre_dir |
+    d sigma] in the gradient rows' padding (layout.h); the activation-mask kernel and the f32 path
+    leave the slots 0 (absent), so the weight gradient finds the maxima itself."""
+    r = _mlp_forward_backward(ref_state, app_vec, R=40, N=64)
+    grad = r["grad"].numpy()
+    slot = 2177
+    if _lib().get_mlp_arith() == "f16x3":
+        slices = [slice(256 * (j + 1), 256 * (j + 2)) for j in range(7)] + [slice(2048, 2177)]
+        np.testing.assert_array_equal(grad[:, slot], block_records(grad, slices))
+    else:
+        assert np.all(grad[:, slot] == 0)
+
+
+def no_worse_on_own_branches(got, f64_got, ref, f64_ref, name, factor=2.0, max_factor=3.0):
+    """got (the GPU) against float64 on the GPU's own ReLU branches is no further than ref (the fp32 CPU
+    autograd) against float64 on the CPU's branches: within `factor` in rel-L2, p99.9 and median, and
+    `max_factor` in the maximum (each entry relative to the tensor's largest float64 entry).
+    Kink-proof as test_gpu_accuracy's gradient test: a pre-activation within rounding of 0 costs each
+    evaluation its rounding, not a jump between the linear pieces of two branches.
+    The factors are the spread between two fp32 evaluations of one size (profiles/r05/
+    pytest_train_tight.log, diag_dir_grads2.log): the data-gradient rows of both GPU arithmetics sit at
+    1.2-1.5x the CPU's error (the MFMA's f32 accumulation is not correctly rounded; the exact-f32 path
+    shows it too); a full step's head gradients (dir_linear, the appearance row) are sums over every
+    sample of rows whose error carries a ~1e-7 mean from the composite's float alphas, which in one
+    512-ray batch landed at 2.2-2.3x the CPU's draw and in the 4,096-ray batch at 1.0-1.1x; and the
+    maximum over 10^5-10^6 entries is one extreme draw (up to 2.1x apart)."""
+    got, f64_got, ref, f64_ref = (np.asarray(t, np.float64).ravel() for t in (got, f64_got, ref, f64_ref))
+    sc = max(np.abs(f64_got).max(), np.abs(f64_ref).max()) + 1e-300
+    eg, er = np.abs(got - f64_got) / sc, np.abs(ref - f64_ref) / sc
+    stats = [("max", np.max, max_factor), ("p99.9", lambda v: np.quantile(v, 0.999), factor), ("median", np.median, factor)]
+    line = [f"{n}: {float(f(eg)):.3g}/{float(f(er)):.3g}" for n, f, _ in stats]
+    line.append(f"rel-L2: {rel_l2(got, f64_got):.3g}/{rel_l2(ref, f64_ref):.3g}")
+    print(f"{name} (gpu/cpu vs float64) " + "  ".join(line))
+    for stat, f, k in stats:
+        assert f(eg) <= k * f(er) + 1e-9, (name, stat, float(f(eg)), float(f(er)))
+    assert rel_l2(got, f64_got) <= factor * rel_l2(ref, f64_ref) + 1e-9, (name, rel_l2(got, f64_got), rel_l2(ref, f64_ref))
+
+
+def gpu_step_masks(tr, o, d, t_rand, app_idx):
+    """The ten ReLU branches (trunk layers 0-7, density, dir_linear; models.py:128-150) the trainer's
+    forward takes on this batch at its current packing: the same kernels on the same inputs
+    (normalise, stratified samples on t_rand, ray features, forward with saves; nerf_train_forward's
+    sequence), read from the saved activations (ReLU output > 0, the mask its backward applies)."""
+    from nerfmi.ray_utils import linspace_table
+    L = _lib()
+    lib, P, s, dev = L.load(), L.ptr, L.stream(), tr.dev
+    N = tr.config.num_samples
+    o = o.reshape(-1, 3).to(dev, torch.float32).contiguous()
+    d = d.reshape(-1, 3).to(dev, torch.float32).contiguous()
+    B = o.shape[0]
+    M = B * N
+    dn, z = torch.empty(B, 3, device=dev), torch.empty(B, N, device=dev)
+    feat, encd = torch.empty(B, 256, device=dev), torch.empty(B, 32, device=dev)
+    rgb, sigma = torch.empty(M, 3, device=dev), torch.empty(M, device=dev)
+    save = torch.empty(L.tile_rows(M), L.SAVE_ROW, device=dev)
+    masks = torch.empty(M, L.MASK_ROW, dtype=torch.int32, device=dev)
+    app, rows = (tr.appearance_embeddings[int(app_idx)].reshape(1, 32), 1) if (tr.n_images and app_idx is not None) \
+        else (None, 0)
+    tr_ = t_rand.to(dev, torch.float32).contiguous()
+    L.check(lib.nerf_normalize_dirs(P(d), B, P(dn), s), "normalize")
+    L.check(lib.nerf_sample_stratified(P(o), P(dn), B, tr.near, tr.far, N, P(linspace_table(N, dev)), 1, P(tr_), 0,
+                                       P(z), None, s), "stratified")
+    L.check(lib.nerf_ray_features_train(P(tr.packed), P(dn), B, P(app), rows, P(feat), P(encd), s), "features")
+    L.check(lib.nerf_mlp_forward_train(P(tr.packed), P(o), P(dn), P(z), B, N, P(feat), P(encd), P(rgb), P(sigma),
+                                       P(save), P(masks), s), "mlp_forward_train")
+    torch.cuda.synchronize()
+    r = L.untile(save.cpu(), M)
+    offs = [0, 256, 512, 768, 1088, 1344, 1600, 1856]
+    return [r[:, a:a + 256] > 0 for a in offs] + [(sigma.cpu() > 0).reshape(M, 1), r[:, 2144:2272] > 0]
+
+
+def step_refs(state, table, app_idx, o, d, target, t_rand, m_gpu):
+    """One training step's gradients at `state` (+ appearance table): the oracle's fp32 autograd (its
+    own branches, recorded), float64 on those branches, and float64 on the GPU's branches m_gpu."""
+    def hook(masks=None, record=None):
+        def relu(pre, i):
+            if record is not None:
+                record.append(pre.detach() > 0)
+            return torch.relu(pre) if masks is None else pre * masks[i].to(pre.dtype)
+        return relu
+
+    def run(dtype, relu):
+        st = {k: v.detach().to(dtype).clone() for k, v in state.items()}
+        tab = None if table is None else table.detach().to(dtype).clone()
+        _, _, g, _ = O.train_step(st, tab, app_idx, o.cpu().to(dtype), d.cpu().to(dtype), target.cpu().to(dtype), 2.0,
+                                  6.0, 64, t_rand.cpu().to(dtype), relu=relu)
+        return {k: v.detach().double().numpy() for k, v in g.items()}
+    m_cpu = []
+    g32 = run(torch.float32, hook(record=m_cpu))
+    return g32, run(torch.float64, hook(masks=m_cpu)), run(torch.float64, hook(masks=m_gpu))
+
+
+def _data_grads(st, r, app, g_rgb, g_sigma, dtype, masks=None, record=None):
+    """d (sum rgb g_rgb + sigma g_sigma) / d pre_l, l = 0..7, of the oracle's NeRF.forward in `dtype` on
+    the points of `r`, on the ReLU branches `masks` (None: its own; `record` collects them)."""
+    sd = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in st.items()}
+    pres = []
+
+    def relu(pre, i):
+        if record is not None:
+            record.append(pre.detach() > 0)
+        return torch.relu(pre) if masks is None else pre * masks[i].to(dtype)
+    with torch.enable_grad():
+        rgb, sigma = O.nerf_forward(sd, r["pts"].to(dtype), r["dexp"].to(dtype), None if app is None else app.to(dtype),
+                                    keep=pres, relu=relu)
+        for t in pres:
+            t.retain_grad()
+        ((rgb * g_rgb.to(dtype)).sum() + (sigma[:, 0] * g_sigma.to(dtype)).sum()).backward()
+    return [t.grad.double().numpy() for t in pres]
+
+
 @pytest.mark.parametrize("with_app", [False, True])
 def test_mlp_backward_matches_autograd(ref_state, app_vec, with_app):
-    r = _mlp_forward_backward(ref_state, app_vec if with_app else None)
+    """The data-gradient rows d pre_0..7 against float64, each fp32 evaluation on its own ReLU branches
+    (the GPU's read from its saved activations): no worse than the fp32 CPU autograd."""
+    app = app_vec if with_app else None
+    R, N = 96, 11
+    draw = _draw(R, N, 3)
+    r = _mlp_forward_backward(ref_state, app, R=R, N=N, draw=draw)
+    g_rgb, g_sigma = draw[3], draw[4]
+    save, M = r["save"].numpy(), R * N
+    offs = [0, 256, 512, 768, 1088, 1344, 1600, 1856]
+    m_gpu = [torch.from_numpy(save[:, o:o + 256] > 0) for o in offs]
+    m_gpu += [(r["sigma"] > 0).reshape(M, 1), torch.from_numpy(save[:, 2144:2272] > 0)]
+    m_cpu = []
+    d32 = _data_grads(ref_state, r, app, g_rgb, g_sigma, torch.float32, record=m_cpu)
+    d64_cpu = _data_grads(ref_state, r, app, g_rgb, g_sigma, torch.float64, masks=m_cpu)
+    d64_gpu = _data_grads(ref_state, r, app, g_rgb, g_sigma, torch.float64, masks=m_gpu)
     grad = r["grad"].numpy()
     for l in range(8):
-        exp = r["pres"][l].grad.numpy()
-        got = grad[:, 256 * l: 256 * (l + 1)]
-        assert rel_l2(got, exp) < 2e-4, (l, rel_l2(got, exp))
-        ok, frac = mostly_close(got, exp)
-        assert ok, (l, frac)
+        no_worse_on_own_branches(grad[:, 256 * l: 256 * (l + 1)], d64_gpu[l], d32[l], d64_cpu[l], f"d pre_{l}")
+
+
+@pytest.mark.parametrize("R,N", [(40, 64), (2048, 64)])
+def test_param_grads_records_match_fallback(ref_state, app_vec, R, N):
+    """The split-f16 weight gradient scales each chunk by its operands' largest exponents, taken from
+    the producers' block records or, with the records absent, found by reading the chunk first.  Both
+    give the same exponents, so every gradient is bit-identical (R = 2048: 1,024-sample chunks)."""
+    L = _lib()
+    lib, dev = L.load(), L.device()
+    r = _mlp_forward_backward(ref_state, app_vec, R=R, N=N)
+    M = R * N
+    packed, _, ts = packed_of(ref_state, dev)
+    a = app_vec.reshape(1, 32).to(dev).contiguous()
+    dapp = torch.empty(1, 32, device=dev)
+    ws = torch.empty(lib.nerf_param_grads_workspace_bytes(M), dtype=torch.uint8, device=dev)
+    outs = []
+    for absent in (False, True):
+        save, grad = r["save_tiled"].to(dev), r["grad_tiled"].to(dev)
+        if absent:   # the record slots (layout.h kMetaSaveF / kMetaGradF) zeroed: "absent"
+            save.view(-1, L.SAVE_ROW // 8, 32, 8)[:, 1087 // 8, :, 1087 % 8] = 0.0
+            grad.view(-1, L.GRAD_ROW // 8, 32, 8)[:, 2177 // 8, :, 2177 % 8] = 0.0
+        grads = [torch.empty_like(t) for t in ts]
+        arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in grads])
+        L.check(lib.nerf_param_grads(L.ptr(save), L.ptr(grad), M, N, L.ptr(a), 1, L.ptr(packed), arr, L.ptr(dapp),
+                                     L.ptr(ws), ws.numel(), L.stream()), "param_grads")
+        torch.cuda.synchronize()
+        outs.append([g.cpu() for g in grads])
+    for k, g1, g2 in zip(O.STATE_KEYS, *outs):
+        assert torch.equal(g1, g2), k
+        assert torch.isfinite(g1).all(), k
 
 
 @pytest.mark.parametrize("with_app", [False, True])
@@ -557,11 +731,19 @@ def test_trainer_matches_oracle_over_steps(ref_state):
                                                optimizer=opt)
         _, _, _, opt64 = O.train_step(st64, tab64, img, o.cpu().double(), d.cpu().double(), target.double(), 2.0, 6.0,
                                       64, t_rand.double(), optimizer=opt64)
+        # this step's gradient references at the GPU's own current parameters (the trajectories part
+        # by Adam's +-lr moves of ~0 gradients): the oracle's fp32 autograd and float64, each fp32
+        # evaluation held to float64 on its own ReLU branches (no_worse_on_own_branches)
+        names = list(O.STATE_KEYS) + ["appearance_embeddings"]
+        cur = {n: tr.view(tr.flat, i).detach().cpu().clone() for i, n in enumerate(names)}
         loss, _ = tr.forward_backward(o, d, target.to(tr.dev), img, t_rand=t_rand)
         assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o), step
-        for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
+        m_gpu = gpu_step_masks(tr, o, d, t_rand, img)
+        g32, g64c, g64g = step_refs({k: cur[k] for k in O.STATE_KEYS}, cur["appearance_embeddings"], img, o, d, target,
+                                    t_rand, m_gpu)
+        for i, n in enumerate(names):
             got = tr.view(tr.grad, i).detach().cpu().numpy()
-            assert rel_l2(got, grads_o[n].numpy()) < 5e-4, (step, n, rel_l2(got, grads_o[n].numpy()))
+            no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], f"step {step} {n}", factor=2.5)
         tr.optimizer_step()
     torch.cuda.synchronize()
     names = list(O.STATE_KEYS) + ["appearance_embeddings"]
@@ -642,9 +824,11 @@ def test_production_batch_matches_oracle(ref_state, app_vec):
     loss, _ = tr.forward_backward(o, d, target.to(tr.dev), 2, t_rand=t_rand)
     torch.cuda.synchronize()
     assert abs(float(loss) - float(loss_o)) <= 2e-5 * float(loss_o)
+    m_gpu = gpu_step_masks(tr, o, d, t_rand, 2)
+    g32, g64c, g64g = step_refs(ref_state, table, 2, o, d, target, t_rand, m_gpu)
     for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
         got = tr.view(tr.grad, i).detach().cpu().numpy()
-        assert rel_l2(got, grads_o[n].numpy()) < 5e-4, (n, rel_l2(got, grads_o[n].numpy()))
+        no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], n, factor=2.5)
 
 
 def test_no_appearance_model_trains_like_the_oracle(noapp_state):
