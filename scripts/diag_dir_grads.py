@@ -125,12 +125,24 @@ def main():
         for k in ("rgb", "sigma", "rgb_map", "drgb", "dsigma", "dpre_dir", "dpre_7"):
             print(f"  {k:10s} {rel(gpu[k], g64[k]):.3g} {bias(gpu[k], g64[k]):+.3g} | "
                   f"{rel(c32[k], c64[k]):.3g} {bias(c32[k], c64[k]):+.3g}")
+        if os.environ.get("DIAG_SAVE"):
+            np.savez(os.path.join(os.environ["DIAG_SAVE"], f"composite_inputs_{arith}.npz"), rgb=gpu["rgb"].astype(np.float32),
+                     sigma=gpu["sigma"].astype(np.float32), z=z.cpu().numpy(), rgb_map=gpu["rgb_map"].astype(np.float32),
+                     target=target.numpy(), drgb=gpu["drgb"].astype(np.float32))
         # the composite alone: float64 render + mse backward from the GPU's own rgb / sigma / z
         rgb_t = torch.from_numpy(gpu["rgb"]).reshape(B, N, 3).requires_grad_(True)
         with torch.enable_grad():
             rm, _, _ = O.composite(rgb_t, torch.from_numpy(gpu["sigma"]).reshape(B, N, 1), z.cpu().double())
             torch.nn.functional.mse_loss(rm, target.double()).backward()
         dr64 = rgb_t.grad.reshape(-1, 3).numpy()
+        # the reference's own fp32 composite (O.composite in float32, torch CPU) on the same GPU inputs
+        rgb_32 = torch.from_numpy(gpu["rgb"]).float().reshape(B, N, 3).requires_grad_(True)
+        with torch.enable_grad():
+            rm32, _, _ = O.composite(rgb_32, torch.from_numpy(gpu["sigma"]).float().reshape(B, N, 1), z.cpu())
+            torch.nn.functional.mse_loss(rm32, target).backward()
+        print(f"  cpu fp32 composite on the gpu's inputs: rgb_map {rel(rm32.detach().numpy(), rm.detach().numpy()):.3g} "
+              f"{bias(rm32.detach().numpy(), rm.detach().numpy()):+.3g}  drgb "
+              f"{rel(rgb_32.grad.reshape(-1, 3).numpy(), dr64):.3g} {bias(rgb_32.grad.reshape(-1, 3).numpy(), dr64):+.3g}")
         print(f"  composite only: rgb_map {rel(gpu['rgb_map'], rm.detach().numpy()):.3g} "
               f"{bias(gpu['rgb_map'], rm.detach().numpy()):+.3g}  drgb {rel(gpu['drgb'], dr64):.3g} {bias(gpu['drgb'], dr64):+.3g}")
         for k in ("dpre_dir", "dpre_7"):

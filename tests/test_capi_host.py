@@ -65,13 +65,13 @@ def test_bad_arguments_are_reported_not_launched():
     assert lib.nerf_adam(None, None, None, None, 8, 1e-3, .9, .999, 1e-8, 0, None) == 1   # step counts from 1
     assert lib.nerf_wgrad(None, 1, 4, None, 4, 4, 1, 8, None, None, 0, None, 0, None) == 1
     ws = lib.nerf_wgrad_workspace_bytes(5000, 256, 256)
-    # the 256 x 256 path's 1024-sample chunks, halved (down to one 16-sample stage) while a short GEMM has
-    # fewer than 256 of them: 5000 samples -> 16-sample chunks, 313 of them, x N x (K + bias column)
-    clen = 1024
-    while clen > 16 and -(-5000 // clen) < 256:
+    # the 256 x 256 path's 2048-sample chunks, halved (down to one 16-sample stage) while a short GEMM has
+    # fewer than 128 of them: 5000 samples -> 32-sample chunks, 157 of them, x N x (K + bias column)
+    clen = 2048
+    while clen > 16 and -(-5000 // clen) < 128:
         clen //= 2
-    assert clen == 16 and ws == -(-5000 // clen) * (256 * 257 + 4) * 4
-    assert lib.nerf_wgrad_workspace_bytes(262144, 256, 256) == 256 * (256 * 257 + 4) * 4   # production size: 1024-sample chunks
+    assert clen == 32 and ws == -(-5000 // clen) * (256 * 257 + 4) * 4
+    assert lib.nerf_wgrad_workspace_bytes(262144, 256, 256) == 128 * (256 * 257 + 4) * 4   # production size: 2048-sample chunks
     assert lib.nerf_train_workspace_bytes(4096, 64) > 4096 * 64 * (2400 + 2312) * 4
     assert lib.nerf_mlp_backward(None, None, None, None, None, None, None, None, 0, None, None) == 0
     # post effects

@@ -329,29 +329,31 @@ def test_gradient_block_records(ref_state, app_vec):
         assert np.all(grad[:, slot] == 0)
 
 
-def no_worse_on_own_branches(got, f64_got, ref, f64_ref, name, factor=2.0, max_factor=3.0):
+def no_worse_on_own_branches(got, f64_got, ref, f64_ref, name, factor=2.0, floor=1e-6):
     """got (the GPU) against float64 on the GPU's own ReLU branches is no further than ref (the fp32 CPU
-    autograd) against float64 on the CPU's branches: within `factor` in rel-L2, p99.9 and median, and
-    `max_factor` in the maximum (each entry relative to the tensor's largest float64 entry).
+    autograd) against float64 on the CPU's branches: within factor x the CPU's + floor in rel-L2 and in
+    the max, p99.9 and median of the per-entry error (relative to the tensor's largest float64 entry):
+    test_gpu_accuracy.py's criterion (2x CPU + 1e-6) applied to every statistic.
     Kink-proof as test_gpu_accuracy's gradient test: a pre-activation within rounding of 0 costs each
     evaluation its rounding, not a jump between the linear pieces of two branches.
-    The factors are the spread between two fp32 evaluations of one size (profiles/r05/
-    pytest_train_tight.log, diag_dir_grads2.log): the data-gradient rows of both GPU arithmetics sit at
-    1.2-1.5x the CPU's error (the MFMA's f32 accumulation is not correctly rounded; the exact-f32 path
-    shows it too); a full step's head gradients (dir_linear, the appearance row) are sums over every
-    sample of rows whose error carries a ~1e-7 mean from the composite's float alphas, which in one
-    512-ray batch landed at 2.2-2.3x the CPU's draw and in the 4,096-ray batch at 1.0-1.1x; and the
-    maximum over 10^5-10^6 entries is one extreme draw (up to 2.1x apart)."""
+    Why a floor (profiles/r05/pytest_train_tight*.log, diag_dir_grads*.log, composite_bias_hosts.log):
+    the data-gradient rows of both GPU arithmetics sit at 1.2-1.5x the CPU's error (the MFMA's f32
+    accumulation is not correctly rounded; the exact-f32 path shows it too), and the head gradients
+    (dir_linear, rgb_linear and appearance_projection biases, the appearance row: sums over every
+    sample of rows) carry the composite's mean error, a draw of the host: on one batch's inputs
+    torch's CPU float exp gave rgb_map a mean error of +6e-8 on the GPU box and +2.6e-6 in the build
+    container, the GPU's correctly rounded exp +2.8e-7 on both.  Such tensors land at 2-4x the CPU's
+    draw, at 1-4e-7 absolute; a real fault (a wrong mask, scale or dropped product) costs >= 1e-5."""
     got, f64_got, ref, f64_ref = (np.asarray(t, np.float64).ravel() for t in (got, f64_got, ref, f64_ref))
     sc = max(np.abs(f64_got).max(), np.abs(f64_ref).max()) + 1e-300
     eg, er = np.abs(got - f64_got) / sc, np.abs(ref - f64_ref) / sc
-    stats = [("max", np.max, max_factor), ("p99.9", lambda v: np.quantile(v, 0.999), factor), ("median", np.median, factor)]
-    line = [f"{n}: {float(f(eg)):.3g}/{float(f(er)):.3g}" for n, f, _ in stats]
+    stats = [("max", np.max), ("p99.9", lambda v: np.quantile(v, 0.999)), ("median", np.median)]
+    line = [f"{n}: {float(f(eg)):.3g}/{float(f(er)):.3g}" for n, f in stats]
     line.append(f"rel-L2: {rel_l2(got, f64_got):.3g}/{rel_l2(ref, f64_ref):.3g}")
     print(f"{name} (gpu/cpu vs float64) " + "  ".join(line))
-    for stat, f, k in stats:
-        assert f(eg) <= k * f(er) + 1e-9, (name, stat, float(f(eg)), float(f(er)))
-    assert rel_l2(got, f64_got) <= factor * rel_l2(ref, f64_ref) + 1e-9, (name, rel_l2(got, f64_got), rel_l2(ref, f64_ref))
+    for stat, f in stats:
+        assert f(eg) <= factor * f(er) + floor, (name, stat, float(f(eg)), float(f(er)))
+    assert rel_l2(got, f64_got) <= factor * rel_l2(ref, f64_ref) + floor, (name, rel_l2(got, f64_got), rel_l2(ref, f64_ref))
 
 
 def gpu_step_masks(tr, o, d, t_rand, app_idx):
@@ -447,6 +449,38 @@ def test_mlp_backward_matches_autograd(ref_state, app_vec, with_app):
     grad = r["grad"].numpy()
     for l in range(8):
         no_worse_on_own_branches(grad[:, 256 * l: 256 * (l + 1)], d64_gpu[l], d32[l], d64_cpu[l], f"d pre_{l}")
+
+
+@pytest.mark.parametrize("variant", ["ungrouped", "tr_loader"])
+def test_weight_gradient_variants_agree(tmp_path, variant):
+    """The hidden layers' split-f16 weight gradients run as one grouped launch with one grouped
+    reduction (train.hip wgrad_h16g_kernel); a child process with NERFMI_WGRAD_GROUP=0 runs them as
+    seven launches with their own reductions: same chunks, same kernel body, same fixed-order
+    reductions, so one production-size step's 25 gradients are bit-identical.  With
+    NERFMI_WGRAD_LOADER=tr (the coalesced-staging A/B kernel, wgrad_h16tr_kernel) the MFMA sums are
+    the same and only the bias columns' double sums run in another order: every weight entry is
+    bit-identical and every entry within one float rounding."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import train_variants
+    ref = train_variants.grads()
+    out = tmp_path / "grads.pt"
+    env = dict(os.environ, **({"NERFMI_WGRAD_GROUP": "0"} if variant == "ungrouped" else {"NERFMI_WGRAD_LOADER": "tr"}))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "train_variants.py"), str(out), _lib().get_mlp_arith()],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert set(got) == set(ref)
+    names = list(O.STATE_KEYS) + ["appearance_embeddings"]
+    for k in ref:
+        name = names[int(k)]
+        if variant == "ungrouped" or name.endswith(".weight"):
+            assert torch.equal(got[k], ref[k]), name
+        else:
+            torch.testing.assert_close(got[k], ref[k], rtol=2.5e-7, atol=1e-30, msg=name)
 
 
 @pytest.mark.parametrize("R,N", [(40, 64), (2048, 64)])
@@ -743,7 +777,7 @@ def test_trainer_matches_oracle_over_steps(ref_state):
                                     t_rand, m_gpu)
         for i, n in enumerate(names):
             got = tr.view(tr.grad, i).detach().cpu().numpy()
-            no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], f"step {step} {n}", factor=2.5)
+            no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], f"step {step} {n}")
         tr.optimizer_step()
     torch.cuda.synchronize()
     names = list(O.STATE_KEYS) + ["appearance_embeddings"]
@@ -828,7 +862,7 @@ def test_production_batch_matches_oracle(ref_state, app_vec):
     g32, g64c, g64g = step_refs(ref_state, table, 2, o, d, target, t_rand, m_gpu)
     for i, n in enumerate(list(O.STATE_KEYS) + ["appearance_embeddings"]):
         got = tr.view(tr.grad, i).detach().cpu().numpy()
-        no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], n, factor=2.5)
+        no_worse_on_own_branches(got, g64g[n], g32[n], g64c[n], n)
 
 
 def test_no_appearance_model_trains_like_the_oracle(noapp_state):
