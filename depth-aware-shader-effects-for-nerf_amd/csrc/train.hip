@@ -2417,222 +2417,6 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   h16w_chunk<BLK, NRT>(a, lda, x, ldx, M, clen, meta, partial, blockIdx.x, As, wmax);
 }
 
-// Several 256 x 256 whole-tile GEMMs of one shape (tile-major rows, row lengths lda / ldx) in one
-// launch: workgroup b runs chunk b % chunks of job b / chunks into that job's partial buffer.  The
-// seven hidden layers' weight gradients then fill the chip without per-layer launch tails, and their
-// reductions run as one launch after (wgrad_reduce_group_kernel).
-constexpr int kMaxGroup = 8;
-struct H16Job {
-  const float* a;
-  const float* x;
-  H16Meta meta;
-  float* partial;
-};
-struct H16Group {
-  H16Job job[kMaxGroup];
-};
-__global__ void __launch_bounds__(256, 1)
-wgrad_h16g_kernel(H16Group grp, int64_t lda, int64_t ldx, int64_t M, int clen, int chunks) {
-  __shared__ __attribute__((aligned(16))) H16Stage As;
-  __shared__ float wmax[4][2];
-  const int j = (int)blockIdx.x / chunks;
-  const H16Job& jb = grp.job[j];
-  h16w_chunk<true, 8>(jb.a, lda, jb.x, ldx, M, clen, jb.meta, jb.partial, (int)blockIdx.x - j * chunks, As, wmax);
-}
-
-// The same GEMM with coalesced staging (tile-major operands only): each lane loads 16-byte pieces
-// (4 features of one sample) so that one load instruction covers 4 feature groups x 8 samples, four
-// 256-byte runs (wgrad_h16w_kernel: one dword per lane, eight 32-byte runs), and 8 loads per lane
-// and stage replace 32.  Both operands are split into sample-major f16 images in LDS and the MFMA
-// fragments (8 consecutive samples of one column per lane) come back by two transposed reads
-// (ds_read_b64_tr_b16) each.  Image rows are 288 f16 (144 dwords, 16 mod 64 banks): a store
-// instruction's 8 rows x 16 dwords and a transposed read's 4 rows x 16 dwords per half-wave each
-// fall on 64 distinct banks.  The bias column is summed per lane over the samples it loads (in
-// double) and the 8 lanes of each column are added in lane order at the end.
-constexpr int kTrRow = 288;
-typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ h16x4 lds_read_tr16(const _Float16* p) {
-  return __builtin_bit_cast(h16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                       (__attribute__((address_space(3))) s16x4*)(const_cast<_Float16*>(p))));
-}
-__device__ __forceinline__ void split4_f16(const f32x4& v, float s, h16x4& hi, h16x4& lo) {
-  typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float x0 = v[2 * p] * s, x1 = v[2 * p + 1] * s;
-    const h16x2 hi2 = {(_Float16)x0, (_Float16)x1};
-    const h16x2 lo2 = __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), x0, x1));
-    hi[2 * p] = hi2[0];
-    hi[2 * p + 1] = hi2[1];
-    lo[2 * p] = lo2[0];
-    lo[2 * p + 1] = lo2[1];
-  }
-}
-template <int NRT = 8>
-__global__ void __launch_bounds__(256, 1)
-wgrad_h16tr_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                   int clen, H16Meta meta, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) _Float16 Img[2][2][2][kBfStage][kTrRow];   // [buffer][a | x][hi, lo][sample][column]
-  __shared__ float wmax[4][2];
-  const int chunk = blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  // load q (0..3) of wave wk: feature groups 8 wk + 4 (q >> 1) + (lane >> 4) (columns cq + 0..3 with
-  // cq = 8 g + 4 (lane & 1)), sample 8 (q & 1) + ((lane >> 1) & 7) of the stage
-  const int ls = (lane >> 1) & 7;
-  const int gq0 = 8 * wk + (lane >> 4);                        // group of loads 0, 1 (+4: loads 2, 3)
-  const uint32_t lvo = 1024u * (uint32_t)gq0 + 32u * (uint32_t)ls + 16u * (uint32_t)(lane & 1);
-  const bool a_keep0 = 8 * gq0 < 32 * NRT, a_keep1 = 8 * (gq0 + 4) < 32 * NRT;   // (NRT < 8: rows past the kept ones unread)
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  f32x4 ra[4][4], rx[4][4];
-  double bacc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t vo = (q >> 1) ? (a_keep1 ? lvo : 0x80000000u) : (a_keep0 ? lvo : 0x80000000u);
-      ra[SET][q] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(ares, (int)vo, (int)(4096 * (q >> 1) + 256 * (q & 1)), kRowLoadAux));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      rx[SET][q] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, (int)lvo, (int)(4096 * (q >> 1) + 256 * (q & 1)), kRowLoadAux));
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using C2 = std::integral_constant<int, 2>;
-
-  int Ea, Ex;
-  h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
-  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
-
-  const int cq = 8 * gq0 + 4 * (lane & 1);                     // first column of loads 0, 1 (+32: loads 2, 3)
-  auto split = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bacc[q >> 1][e] += (double)ra[SET][q][e];
-      h16x4 hi, lo;
-      const int row = 8 * (q & 1) + ls, col = cq + 32 * (q >> 1);
-      split4_f16(ra[SET][q], sa, hi, lo);
-      *reinterpret_cast<h16x4*>(&Img[buf][0][0][row][col]) = hi;
-      *reinterpret_cast<h16x4*>(&Img[buf][0][1][row][col]) = lo;
-      split4_f16(rx[SET][q], sx, hi, lo);
-      *reinterpret_cast<h16x4*>(&Img[buf][1][0][row][col]) = hi;
-      *reinterpret_cast<h16x4*>(&Img[buf][1][1][row][col]) = lo;
-    }
-  };
-  // fragment of samples 8h .. 8h+7 of column col0 + c: two transposed 4 x 16 blocks
-  const int trow = 8 * h + ((lane & 15) >> 2), tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  auto frag = [&](int buf, int op, int part, int col0) __attribute__((always_inline)) {
-    const _Float16* p = &Img[buf][op][part][trow][col0 + tcol];
-    const h16x4 lo = lds_read_tr16(p), hi = lds_read_tr16(p + 4 * kTrRow);
-    return h16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  f32x16 acc[NRT][2];
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;
-  load(C0{}, 0);
-  load(C1{}, 1);
-  load(C2{}, 2);
-  split(C0{}, 0);
-  __syncthreads();
-  // iteration st (set st % 4, buffer st % 2): stage st+3's loads; stage st's MFMAs with stage st+1's
-  // split in their shadow; barrier
-  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value, FB = SET & 1;
-    using Nxt = std::integral_constant<int, (SET + 1) & 3>;
-    using Ld = std::integral_constant<int, (SET + 3) & 3>;
-    load(Ld{}, st + 3);
-    __builtin_amdgcn_sched_barrier(0);
-    h16x8 fx[2][2], fa[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fx[j][p] = frag(FB, 1, p, 64 * wk + 32 * j);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) fa[0][p] = frag(FB, 0, p, 0);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 1 < NRT) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) fa[(i + 1) & 1][p] = frag(FB, 0, p, 32 * (i + 1));
-      }
-      const h16x8 (&f)[2] = fa[i & 1];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma16(f[1], fx[j][0], t);
-        t = mfma16(f[0], fx[j][1], t);
-        acc[i][j] = mfma16(f[0], fx[j][0], t);
-      }
-    }
-    split(Nxt{}, FB ^ 1);
-    // schedule: the x fragments' and tile 0's reads, then per row tile the next tile's 4 reads and
-    // its 6 MFMAs, each followed by VALU of the next stage's split; the split's LDS writes last
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 3, 0);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x200, 16, 0);
-    __syncthreads();
-  };
-  for (int st = 0; st < nstages; st += 4) {
-    iteration(C0{}, st);
-    iteration(C1{}, st + 1);
-    iteration(C2{}, st + 2);
-    iteration(std::integral_constant<int, 3>{}, st + 3);
-  }
-  constexpr int KP = kWT + 1;
-  const int64_t stride = wgrad_stride(32 * NRT, kWT);
-  float* out = partial + (size_t)chunk * stride;
-#pragma unroll
-  for (int i = 0; i < NRT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-    }
-  // bias column: column f's 8 lane sums (lanes of one wave, ls = 0..7) added in ls order (the images
-  // are free after the loop's last barrier)
-  double* bsum = reinterpret_cast<double*>(&Img[0][0][0][0][0]);   // [column][ls]
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bsum[(cq + 32 * k + e) * 8 + ls] = bacc[k][e];
-  __syncthreads();
-  if (tid < 32 * NRT) {
-    double b = bsum[tid * 8];
-#pragma unroll
-    for (int l = 1; l < 8; ++l) b += bsum[tid * 8 + l];
-    out[(size_t)tid * KP + kWT] = (float)b;
-  }
-  if (tid == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
-}
-
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2965,21 +2749,6 @@ wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K,
                     float* __restrict__ out_b, int accumulate, WgradSplit split, int scaled) {
   wgrad_reduce_body(partial, chunks, N, K, out_w, ldo, out_b, accumulate, split, scaled);
 }
-// the reductions of a wgrad_h16g_kernel group (blockIdx.y: the job; written, not accumulated)
-struct RedJob {
-  const float* partial;
-  float* out_w;
-  float* out_b;
-  int ldo;
-};
-struct RedGroup {
-  RedJob job[kMaxGroup];
-};
-__global__ void __launch_bounds__(64 * kRedParts)
-wgrad_reduce_group_kernel(RedGroup grp, int chunks, int N, int K, int scaled) {
-  const RedJob& r = grp.job[blockIdx.y];
-  wgrad_reduce_body(r.partial, chunks, N, K, r.out_w, r.ldo, r.out_b, 0, WgradSplit{}, scaled);
-}
 
 size_t wgrad_workspace_floats(int64_t M, int N, int K) {
   const int clen = wgrad_chunk_len(N, K, M);   // >= the chunk count of every path of launch_wgrad
@@ -3040,24 +2809,6 @@ static bool wgrad_h16() {
   }();
   return on;
 }
-// NERFMI_WGRAD_GROUP=0: the hidden layers' split-f16 weight gradients as seven launches (each with
-// its reduction) over two streams instead of one grouped launch (A/B).
-static bool wgrad_group() {
-  static const bool on = [] {
-    const char* e = getenv("NERFMI_WGRAD_GROUP");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-// NERFMI_WGRAD_LOADER=tr: the whole-tile split-f16 GEMMs stage through wgrad_h16tr_kernel's coalesced
-// 16-byte loads (A/B against wgrad_h16w_kernel's dword loads).
-static bool wgrad_tr() {
-  static const bool on = [] {
-    const char* e = getenv("NERFMI_WGRAD_LOADER");
-    return e && strcmp(e, "tr") == 0;
-  }();
-  return on;
-}
 
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
@@ -3083,9 +2834,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     chunks = (int)((M + clen - 1) / clen);
     const bool h16 = wgrad_h16();
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      if (h16 && wgrad_tr())
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (h16)
+      if (h16)
         hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                            hm, ws);
       else
@@ -3094,9 +2843,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
       rc = check_launch("wgrad whole-tile <5>");
       scaled = h16;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
-      if (tiled && wgrad_tr())
-        hipLaunchKernelGGL(wgrad_h16tr_kernel<8>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (tiled)
+      if (tiled)
         hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       else
         hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
@@ -3279,15 +3026,9 @@ static size_t wgrad_stream_floats(int64_t M) {
   }
   return m;
 }
-// one hidden layer's partial buffer (the grouped launch holds seven at once)
-static size_t wgrad_tile_floats(int64_t M) { return (wgrad_workspace_floats(M, kHidden, kHidden) + 63) & ~(size_t)63; }
-constexpr int kGroupJobs = 7;   // hidden layers 1..7
-// param_grads' workspace: two streams' partial buffers (the first holding the grouped launch's seven)
-// + the ray-sum buffers
+// param_grads' workspace: two streams' partial buffers + the ray-sum buffers
 static size_t max_wgrad_floats(int64_t M) {
-  const size_t w1 = (wgrad_stream_floats(M) + 63) & ~(size_t)63;
-  const size_t grouped = kGroupJobs * wgrad_tile_floats(M) + w1;
-  return (grouped > 2 * w1 ? grouped : 2 * w1) + ray_sum_floats(M) + 64;
+  return 2 * ((wgrad_stream_floats(M) + 63) & ~(size_t)63) + ray_sum_floats(M) + 64;
 }
 
 // Which MLP arithmetic the last nerf_train_forward on a workspace ran under (the f32 forward writes no
@@ -3455,7 +3196,7 @@ static H16Meta block_exps(const float* save, const float* grad, int ja, int jx) 
 // buffers at `rays` (N >= kRaySumMinN).
 static int param_grads_jobs(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
                             const float* packed, float* const* g, float* dapp, float* wa, float* wb, size_t wfl,
-                            float* rays, hipStream_t sa, hipStream_t sb, bool grouped = false) {
+                            float* rays, hipStream_t sa, hipStream_t sb) {
   // Job: columns [k0, k0 + K) of parameter p's weight gradient (row length ldo) from x; the bias
   // gradient with the first column block only.  The skip layer's [h3 | enc_x] runs as a 256 x 256
   // block (the whole-tile kernel) plus the 63 PE columns, instead of one 256 x 319 GEMM on 128 x 128
@@ -3479,29 +3220,6 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
-  if (grouped) {   // hidden layers 1..7: one launch on stream A into seven partial buffers at wa, one reduction
-    const int clen = wgrad_chunk_len(kHidden, kHidden, M);
-    const int chunks = (int)((M + clen - 1) / clen);
-    const size_t wt = wgrad_tile_floats(M);
-    H16Group grp{};
-    RedGroup red{};
-    int n = 0;
-    for (const Job& j : jobs) {
-      if (!(j.n == kHidden && j.K == kHidden)) continue;
-      float* part = wa + (size_t)n * wt;
-      grp.job[n] = H16Job{grad + tile_col(j.a), save + tile_col(j.x), block_exps(save, grad, j.ja, j.jx), part};
-      red.job[n] = RedJob{part, g[j.p] + j.k0, g[j.p + 1], j.ldo};
-      ++n;
-    }
-    if (n != kGroupJobs) return set_error(NERF_ERR_UNSUPPORTED, "param_grads: %d grouped jobs", n);
-    hipLaunchKernelGGL(wgrad_h16g_kernel, dim3((unsigned)(chunks * n)), dim3(256), 0, sa, grp, (int64_t)kGradRow,
-                       (int64_t)kSaveRow, M, clen, chunks);
-    if ((rc = check_launch("wgrad_h16g_kernel"))) return rc;
-    const int64_t cols4 = wgrad_stride(kHidden, kHidden) / 4;
-    hipLaunchKernelGGL(wgrad_reduce_group_kernel, dim3((unsigned)((cols4 + 63) / 64), (unsigned)n), dim3(64 * kRedParts), 0,
-                       sa, red, chunks, kHidden, kHidden, 1);
-    if ((rc = check_launch("wgrad_reduce_group_kernel"))) return rc;
-  }
 #ifndef NERF_PE_SEPARATE   // (A/B build: layer 0 and the skip PE columns as two K = 63 launches)
   if ((rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
 #endif
@@ -3509,13 +3227,11 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
 #ifndef NERF_PE_SEPARATE
     if (j.K == kPosEnc) continue;            // (in the pair above)
 #endif
-    if (grouped && j.n == kHidden && j.K == kHidden) continue;   // (in the group above)
     if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
 #ifndef NERF_HEAD3_GEMM   // (A/B build: the rgb head on the 128 x 128 tile GEMM)
     if (j.a == kGradRgb) {   // the rgb head: the streaming kernel (3 rows)
-      const bool on_b = j.b || grouped;   // (grouped: stream A's buffer holds the group's partials)
       if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
-                                   on_b ? wb : wa, wfl, on_b ? sb : sa)))
+                                   j.b ? wb : wa, wfl, j.b ? sb : sa)))
         return rc;
       continue;
     }
@@ -3599,17 +3315,12 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   const bool two = false;
 #endif
   if (!two) return param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws, avail, rays, s, s);
-  // the grouped hidden-layer launch (split-f16 weight gradients): stream A's buffer holds its seven
-  // partials, stream B's follows
-  const size_t wg = kGroupJobs * wgrad_tile_floats(M);
-  const bool grouped = g_mlp_arith == NERF_ARITH_F16X3 && wgrad_h16() && !wgrad_tr() && wgrad_group() && avail >= wg + w1;
   PgStreams* ps;
   int rc;
   if ((rc = pg_streams(&ps))) return rc;
   if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->s2, ps->fork, 0) != hipSuccess)
     return set_error(NERF_ERR_HIP, "param_grads: stream fork failed");
-  rc = grouped ? param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + wg, w1, rays, s, ps->s2, true)
-               : param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2);
+  rc = param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2);
   // join even after a failed launch, so the caller's stream never runs ahead of queued work
   if (hipEventRecord(ps->join, ps->s2) != hipSuccess || hipStreamWaitEvent(s, ps->join, 0) != hipSuccess)
     return rc ? rc : set_error(NERF_ERR_HIP, "param_grads: stream join failed");
