@@ -2439,205 +2439,6 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   h16w_chunk<BLK, NRT>(a, lda, x, ldx, M, clen, meta, partial, blockIdx.x, As, wmax);
 }
 
-// The same GEMM with coalesced staging (tile-major operands only): each lane loads 16-byte pieces
-// (4 features of one sample) so that one load instruction covers 4 feature groups x 8 samples, four
-// 256-byte runs (wgrad_h16w_kernel: one dword per lane, eight 32-byte runs), and 8 loads per lane
-// and stage replace 32.  Both operands are split into sample-major f16 images in LDS and the MFMA
-// fragments (8 consecutive samples of one column per lane) come back by two transposed reads
-// (ds_read_b64_tr_b16) each.  Image rows are 288 f16 (144 dwords, 16 mod 64 banks): a store
-// instruction's 8 rows x 16 dwords and a transposed read's 4 rows x 16 dwords per half-wave each
-// fall on 64 distinct banks.  The bias column is summed per lane over the samples it loads (in
-// double) and the 8 lanes of each column are added in lane order at the end.
-constexpr int kTrRow = 288;
-typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ h16x4 lds_read_tr16(const _Float16* p) {
-  return __builtin_bit_cast(h16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                       (__attribute__((address_space(3))) s16x4*)(const_cast<_Float16*>(p))));
-}
-__device__ __forceinline__ void split4_f16(const f32x4& v, float s, h16x4& hi, h16x4& lo) {
-  typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float x0 = v[2 * p] * s, x1 = v[2 * p + 1] * s;
-    const h16x2 hi2 = {(_Float16)x0, (_Float16)x1};
-    const h16x2 lo2 = __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), x0, x1));
-    hi[2 * p] = hi2[0];
-    hi[2 * p + 1] = hi2[1];
-    lo[2 * p] = lo2[0];
-    lo[2 * p + 1] = lo2[1];
-  }
-}
-template <int NRT, int NS>
-__global__ void __launch_bounds__(256, 1)
-wgrad_h16tr_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                   int clen, H16Meta meta, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) _Float16 Img[2][2][2][kBfStage][kTrRow];   // [buffer][a | x][hi, lo][sample][column]
-  __shared__ float wmax[4][2];
-  const int chunk = blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  // load q (0..3) of wave wk: feature groups 8 wk + 4 (q >> 1) + (lane >> 4) (columns cq + 0..3 with
-  // cq = 8 g + 4 (lane & 1)), sample 8 (q & 1) + ((lane >> 1) & 7) of the stage
-  const int ls = (lane >> 1) & 7;
-  const int gq0 = 8 * wk + (lane >> 4);                        // group of loads 0, 1 (+4: loads 2, 3)
-  const uint32_t lvo = 1024u * (uint32_t)gq0 + 32u * (uint32_t)ls + 16u * (uint32_t)(lane & 1);
-  const bool a_keep0 = 8 * gq0 < 32 * NRT, a_keep1 = 8 * (gq0 + 4) < 32 * NRT;   // (NRT < 8: rows past the kept ones unread)
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  f32x4 ra[NS][4], rx[NS][4];      // NS sets of raw operands: loads run NS - 1 stages ahead
-  double bacc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t vo = (q >> 1) ? (a_keep1 ? lvo : 0x80000000u) : (a_keep0 ? lvo : 0x80000000u);
-      ra[SET][q] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(ares, (int)vo, (int)(4096 * (q >> 1) + 256 * (q & 1)), kRowLoadAux));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      rx[SET][q] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, (int)lvo, (int)(4096 * (q >> 1) + 256 * (q & 1)), kRowLoadAux));
-  };
-
-  int Ea, Ex;
-  h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
-  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
-
-  const int cq = 8 * gq0 + 4 * (lane & 1);                     // first column of loads 0, 1 (+32: loads 2, 3)
-  auto split = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bacc[q >> 1][e] += (double)ra[SET][q][e];
-      h16x4 hi, lo;
-      const int row = 8 * (q & 1) + ls, col = cq + 32 * (q >> 1);
-      split4_f16(ra[SET][q], sa, hi, lo);
-      *reinterpret_cast<h16x4*>(&Img[buf][0][0][row][col]) = hi;
-      *reinterpret_cast<h16x4*>(&Img[buf][0][1][row][col]) = lo;
-      split4_f16(rx[SET][q], sx, hi, lo);
-      *reinterpret_cast<h16x4*>(&Img[buf][1][0][row][col]) = hi;
-      *reinterpret_cast<h16x4*>(&Img[buf][1][1][row][col]) = lo;
-    }
-  };
-  // fragment of samples 8h .. 8h+7 of column col0 + c: two transposed 4 x 16 blocks
-  const int trow = 8 * h + ((lane & 15) >> 2), tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  auto frag = [&](int buf, int op, int part, int col0) __attribute__((always_inline)) {
-    const _Float16* p = &Img[buf][op][part][trow][col0 + tcol];
-    const h16x4 lo = lds_read_tr16(p), hi = lds_read_tr16(p + 4 * kTrRow);
-    return h16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  f32x16 acc[NRT][2];
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  const int nstages = (int)((mrel_end + kBfStage - 1) / kBfStage);
-#pragma unroll
-  for (int q = 0; q + 1 < NS; ++q) {
-    if (q == 0) load(std::integral_constant<int, 0>{}, 0);
-    if (q == 1) load(std::integral_constant<int, (NS > 1 ? 1 : 0)>{}, 1);
-    if (q == 2) load(std::integral_constant<int, (NS > 2 ? 2 : 0)>{}, 2);
-    if (q == 3) load(std::integral_constant<int, (NS > 3 ? 3 : 0)>{}, 3);
-    if (q == 4) load(std::integral_constant<int, (NS > 4 ? 4 : 0)>{}, 4);
-  }
-  split(std::integral_constant<int, 0>{}, 0);
-  __syncthreads();
-  // iteration st (IT = st mod the unroll U: set IT % NS, buffer IT % 2): stage st+NS-1's loads; stage
-  // st's MFMAs with stage st+1's split in their shadow; barrier
-  auto iteration = [&](auto it_c, int st) __attribute__((always_inline)) {
-    constexpr int IT = decltype(it_c)::value, SET = IT % NS, FB = IT & 1;
-    using Nxt = std::integral_constant<int, (IT + 1) % NS>;
-    using Ld = std::integral_constant<int, (IT + NS - 1) % NS>;
-    load(Ld{}, st + NS - 1);
-    __builtin_amdgcn_sched_barrier(0);
-    h16x8 fx[2][2], fa[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fx[j][p] = frag(FB, 1, p, 64 * wk + 32 * j);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) fa[0][p] = frag(FB, 0, p, 0);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 1 < NRT) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) fa[(i + 1) & 1][p] = frag(FB, 0, p, 32 * (i + 1));
-      }
-      const h16x8 (&f)[2] = fa[i & 1];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma16(f[1], fx[j][0], t);
-        t = mfma16(f[0], fx[j][1], t);
-        acc[i][j] = mfma16(f[0], fx[j][0], t);
-      }
-    }
-    split(Nxt{}, FB ^ 1);
-    // schedule: the x fragments' and tile 0's reads, then per row tile the next tile's 4 reads and
-    // its 6 MFMAs, each followed by VALU of the next stage's split; the split's LDS writes last
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 3, 0);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x200, 16, 0);
-    __syncthreads();
-  };
-  constexpr int U = NS % 2 ? 2 * NS : NS;
-#define NERF_TR_IT(I) \
-  if constexpr (I < U) iteration(std::integral_constant<int, (I < U ? I : 0)>{}, st + I);
-  // (stages past the chunk load nothing and add zeros: nstages rounds up to the unroll)
-  for (int st = 0; st < nstages; st += U) {
-    NERF_TR_IT(0) NERF_TR_IT(1) NERF_TR_IT(2) NERF_TR_IT(3) NERF_TR_IT(4)
-    NERF_TR_IT(5) NERF_TR_IT(6) NERF_TR_IT(7) NERF_TR_IT(8) NERF_TR_IT(9)
-  }
-#undef NERF_TR_IT
-  static_assert(NS >= 3 && NS <= 5, "2..4 stages of loads in flight");
-  constexpr int KP = kWT + 1;
-  const int64_t stride = wgrad_stride(32 * NRT, kWT);
-  float* out = partial + (size_t)chunk * stride;
-#pragma unroll
-  for (int i = 0; i < NRT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-    }
-  // bias column: column f's 8 lane sums (lanes of one wave, ls = 0..7) added in ls order (the images
-  // are free after the loop's last barrier)
-  double* bsum = reinterpret_cast<double*>(&Img[0][0][0][0][0]);   // [column][ls]
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bsum[(cq + 32 * k + e) * 8 + ls] = bacc[k][e];
-  __syncthreads();
-  if (tid < 32 * NRT) {
-    double b = bsum[tid * 8];
-#pragma unroll
-    for (int l = 1; l < 8; ++l) b += bsum[tid * 8 + l];
-    out[(size_t)tid * KP + kWT] = (float)b;
-  }
-  if (tid == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
-}
-
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -3030,19 +2831,6 @@ static bool wgrad_h16() {
   }();
   return on;
 }
-// NERFMI_WGRAD_LOADER=tr3|tr4|tr5: the whole-tile split-f16 GEMMs stage through wgrad_h16tr_kernel's
-// coalesced 16-byte loads with 2..4 stages of loads in flight (A/B against wgrad_h16w_kernel)
-static int wgrad_tr() {
-  static const int ns = [] {
-    const char* e = getenv("NERFMI_WGRAD_LOADER");
-    if (!e) return 0;
-    if (strcmp(e, "tr3") == 0) return 3;
-    if (strcmp(e, "tr4") == 0) return 4;
-    if (strcmp(e, "tr5") == 0) return 5;
-    return 0;
-  }();
-  return ns;
-}
 
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
@@ -3068,13 +2856,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     chunks = (int)((M + clen - 1) / clen);
     const bool h16 = wgrad_h16();
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      if (h16 && wgrad_tr() == 3)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<5, 3>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (h16 && wgrad_tr() == 4)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<5, 4>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (h16 && wgrad_tr() == 5)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<5, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (h16)
+      if (h16)
         hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                            hm, ws);
       else
@@ -3083,13 +2865,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
       rc = check_launch("wgrad whole-tile <5>");
       scaled = h16;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
-      if (tiled && wgrad_tr() == 3)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<8, 3>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (tiled && wgrad_tr() == 4)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<8, 4>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (tiled && wgrad_tr() == 5)
-        hipLaunchKernelGGL((wgrad_h16tr_kernel<8, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else if (tiled)
+      if (tiled)
         hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       else
         hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
