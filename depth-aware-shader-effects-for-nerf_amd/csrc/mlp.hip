@@ -363,22 +363,27 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
 // -------------------------------------------------------------------------- ray features
 // Per ray: feat[0:128] = dir_linear.bias + dir_linear.weight[:,256:283] . PE_4(d)
 //          feat[128:256] = appearance_projection(app) or 0.
-// A block handles 64 rays: the 64x27 direction encodings and 64x32 appearance rows are
-// staged in LDS, then thread n holds row n of its weight matrix in registers and computes output
-// n for all 64 rays (LDS broadcast reads, coalesced 1 KiB stores per ray).  (16 rays per block
-// re-read the weight rows, strided across threads, every 16 rays: 0.38 ms for the 800^2 frame's
-// 640,000 rays, 1.7 TB/s.)
+// A block handles kFeatRays = 64 rays: the 64x27 direction encodings and 64x32 appearance rows
+// are staged in LDS, then thread n holds row n of its weight matrix in registers and computes
+// output n for all 64 rays (LDS broadcast reads, coalesced 1 KiB stores per ray).  (16 rays per
+// block re-read the weight rows, strided across threads, every 16 rays: 0.38 ms for the 800^2
+// frame's 640,000 rays, 1.7 TB/s.)  A small batch (the training step's 4,096 rays: 64 blocks, each
+// thread's 64-ray chain latency-bound, 23 us) runs 16 rays per block instead: 4x the blocks, a
+// quarter of the chain, the same fmaf order per output (bit-identical).
 constexpr int kFeatRays = 64;
+constexpr int kFeatRaysSmall = 16;
+constexpr int64_t kFeatSmallMaxRays = 65536;   // up to 4,096 blocks of 16 rays
 
+template <int RAYS>
 __global__ void __launch_bounds__(256)
 ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ dirs, int64_t R,
                     const float* __restrict__ app, int64_t app_rows, float* __restrict__ feat,
                     float* __restrict__ encd) {
-  __shared__ float enc[kFeatRays][kDirEnc + 1];
-  __shared__ float apps[kFeatRays][kAppDim];
+  __shared__ float enc[RAYS][kDirEnc + 1];
+  __shared__ float apps[RAYS][kAppDim];
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * kFeatRays;
-  for (int q = tid; q < kFeatRays * 3 * kDirLevels; q += 256) {
+  const int64_t r0 = (int64_t)blockIdx.x * RAYS;
+  for (int q = tid; q < RAYS * 3 * kDirLevels; q += 256) {
     const int ray = q / (3 * kDirLevels), ic = q % (3 * kDirLevels);
     const int i = ic / 3, c = ic % 3;
     const int64_t r = imin64(r0 + ray, R - 1);
@@ -387,12 +392,12 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
     enc[ray][3 + 6 * i + c] = sn;
     enc[ray][6 + 6 * i + c] = cs;
   }
-  if (tid < kFeatRays * 3) {
+  if (tid < RAYS * 3) {
     const int ray = tid / 3, c = tid % 3;
     enc[ray][c] = dirs[3 * imin64(r0 + ray, R - 1) + c];
   }
   if (app_rows > 0) {
-    for (int q = tid; q < kFeatRays * kAppDim; q += 256) {
+    for (int q = tid; q < RAYS * kAppDim; q += 256) {
       const int ray = q / kAppDim, k = q % kAppDim;
       const int64_t row = app_rows == 1 ? 0 : imin64(r0 + ray, R - 1);
       apps[ray][k] = app[row * kAppDim + k];
@@ -400,20 +405,20 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
   }
   __syncthreads();
   if (encd) {   // training: each ray's PE_4(d), padded to 32
-    for (int q = tid; q < kFeatRays * 32; q += 256) {
+    for (int q = tid; q < RAYS * 32; q += 256) {
       const int ray = q / 32, k = q % 32;
       if (r0 + ray < R) encd[(r0 + ray) * 32 + k] = k < kDirEnc ? enc[ray][k] : 0.0f;
     }
   }
   const int n = tid;
-  const int nr = (int)imin64(kFeatRays, R - r0);
+  const int nr = (int)imin64(RAYS, R - r0);
   // the same fmaf chain per output as before: b, then k = 0, 1, ... in order
   if (n < kDirHidden) {
     float w[kDirEnc];
 #pragma unroll
     for (int k = 0; k < kDirEnc; ++k) w[k] = packed[kOffDirWd + n * kDirEnc + k];
     const float b = packed[kOffDirB + n];
-    for (int ray = 0; ray < kFeatRays; ray += 4) {   // 4 independent chains (rows past R: garbage, not stored)
+    for (int ray = 0; ray < RAYS; ray += 4) {   // 4 independent chains (rows past R: garbage, not stored)
       float acc[4] = {b, b, b, b};
 #pragma unroll
       for (int k = 0; k < kDirEnc; ++k)
@@ -430,7 +435,7 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
       float w[kAppDim];
 #pragma unroll
       for (int k = 0; k < kAppDim; ++k) w[k] = packed[kOffAppW + m * kAppDim + k];
-      for (int ray = 0; ray < kFeatRays; ray += 4) {
+      for (int ray = 0; ray < RAYS; ray += 4) {
         float acc[4] = {b, b, b, b};
 #pragma unroll
         for (int k = 0; k < kAppDim; ++k)
@@ -449,8 +454,12 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
                         int64_t app_rows, float* feat, hipStream_t s, float* encd) {
   if (R == 0) return NERF_OK;
-  hipLaunchKernelGGL(ray_features_kernel, dim3((unsigned)((R + kFeatRays - 1) / kFeatRays)), dim3(256), 0, s,
-                     packed, dirs, R, app, app_rows, feat, encd);
+  if (R <= kFeatSmallMaxRays)
+    hipLaunchKernelGGL(ray_features_kernel<kFeatRaysSmall>, dim3((unsigned)((R + kFeatRaysSmall - 1) / kFeatRaysSmall)),
+                       dim3(256), 0, s, packed, dirs, R, app, app_rows, feat, encd);
+  else
+    hipLaunchKernelGGL(ray_features_kernel<kFeatRays>, dim3((unsigned)((R + kFeatRays - 1) / kFeatRays)), dim3(256), 0,
+                       s, packed, dirs, R, app, app_rows, feat, encd);
   return check_launch("ray_features_kernel");
 }
 

@@ -153,6 +153,9 @@ class Trainer:
         self._side.wait_event(self._fork)
         _lib.check(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), self._side.cuda_stream),
                    "nerf_pack_weights_transposed")
+        if self.app_grad is not None:    # the table's gradient is one row this step: zeroed beside the forward
+            with torch.cuda.stream(self._side):
+                self.app_grad.zero_()
         self._join.record(self._side)
         if N not in self._tvals:
             self._tvals[N] = linspace_table(N, self.dev)
@@ -169,15 +172,12 @@ class Trainer:
                    "nerf_train_forward")
         if _marks is not None:
             _marks[1].record(torch.cuda.current_stream())
-        if self.app_grad is not None:
-            self.app_grad.zero_()
-        dapp = self.dapp if rows else None
+        # d app of the batch's image goes straight into its row of the table's gradient
+        dapp = self.app_grad[int(app_idx)] if rows else None
         main.wait_event(self._join)
         _lib.check(lib.nerf_train_backward(P(self.packed), P(self.packedT), P(rgb_map), P(tgt), B, N, P(app), rows,
                                            self.grad_ptrs, P(dapp), P(self.loss_buf), P(ws), ws.numel(), s),
                    "nerf_train_backward")
-        if rows:
-            self.app_grad[int(app_idx)].copy_(self.dapp[0])
         if rows == 0:   # appearance_projection unused: its gradient is zero, as torch leaves it (None → no update)
             self.view(self.grad, 20).zero_()
             self.view(self.grad, 21).zero_()
