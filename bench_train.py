@@ -19,7 +19,10 @@ Rank 0 prints one JSON line; value = rays trained per second over all ranks (wea
 
 roofline: per-sample algorithmic FLOP of the three MFMA kernels (forward 1,048,832; data
 gradients 983,040; weight gradients 1,066,752 including bias columns — DESIGN.md §Training)
-over their event-timed durations.  The forward runs on the MLP arithmetic selected by --arith
+over their event-timed durations; for the weight-gradient phase, whose every operand row is
+streamed once, the binding roofline is HBM when its algorithmic bytes (18,188 per sample) at
+8 TB/s take longer than its MFMA work at peak: then bound "hbm" in GB/s, the MFMA figures under
+"mfma".  The forward runs on the MLP arithmetic selected by --arith
 (f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
 157.3).  Under f16x3 the data gradients run on split-f16 MFMA too (838.9) and the weight
 gradients on block-scaled split-f16 MFMA (three f16 products per fp32 product at per-chunk
@@ -51,6 +54,12 @@ FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 
 # 2516.8/3 = 838.9 TFLOP/s; vendor f16 GEMM 1,323.5 / 3); NERFMI_WGRAD=bf16x6 restores the bf16x6
 # GEMMs (six bf16 products: 2516.8/6 = 419.5 TFLOP/s; vendor bf16 1,377.1 / 6).  The layer-0 and
 # skip-PE GEMMs (K = 63) stay bf16x6 either way.
+# HBM: bytes the weight-gradient phase must read once per sample (fp32 rows, layout.h): gradient rows
+# d pre_0..7 (8 x 256), [d pre_dir | d sigma] (129), d hd (128), d rgb (3); saved rows enc_x (63),
+# h_0..h_7 (8 x 256), hd (128).  Against 8 TB/s this is the phase's binding roofline under f16x3
+# (0.60 ms per 262,144 samples, against 0.33 ms of MFMA work at 838.9 TFLOP/s).
+HBM_PEAK_GBS = 8000.0
+WGRAD_ALG_BYTES = 4 * (8 * 256 + 129 + 128 + 3 + 63 + 8 * 256 + 128)   # 18,188
 if os.environ.get("NERFMI_WGRAD") == "bf16x6":
     WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "bf16x6", 6, 1377.1 / 6
 else:
@@ -230,6 +239,16 @@ def measure(args, world, rank, group, ranks):
         dominant = max(kern, key=lambda k: kern[k][1])
         flop, ms = kern[dominant]
         ach = M * flop / (ms * 1e-3) / 1e12
+        # the binding roofline of the dominant phase: MFMA time at peak against HBM time at peak (the
+        # weight gradients stream every saved and gradient row once)
+        hbm = None
+        if dominant == "wgrad":
+            t_mfma = M * flop / (peaks[dominant] * 1e12)
+            t_hbm = M * WGRAD_ALG_BYTES / (HBM_PEAK_GBS * 1e9)
+            if t_hbm > t_mfma:
+                hbm = {"bound": "hbm", "achieved": M * WGRAD_ALG_BYTES / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": M * WGRAD_ALG_BYTES / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "alg_bytes_per_sample": WGRAD_ALG_BYTES, "roofline_ms": {"hbm": t_hbm * 1e3, "mfma": t_mfma * 1e3}}
         traffic = pmc_traffic() if args.arith == "f16x3" else {}
         out = {"metric": "training rays/sec, 4096-ray batches, 64 samples, fwd+bwd+Adam (BASELINE config 5)",
                "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "ranks": ranks,
@@ -248,6 +267,9 @@ def measure(args, world, rank, group, ranks):
                "mlp_arith_forward": args.arith,
                "roofline": {"bound": "mfma", "kernel": dominant, "achieved": ach, "peak": peaks[dominant],
                             "unit": "TFLOP/s", "frac": ach / peaks[dominant],
+                            **(hbm or {}),
+                            **({"mfma": {"achieved": ach, "peak": peaks[dominant], "unit": "TFLOP/s",
+                                         "frac": ach / peaks[dominant]}} if hbm else {}),
                             "traffic": traffic.get(dominant), "traffic_unit": "bytes/phase (one step)",
                             "traffic_source": os.path.relpath(PMC_SUMMARY, os.path.dirname(os.path.abspath(__file__)))
                             if traffic.get(dominant) is not None else None,
