@@ -2439,6 +2439,151 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   h16w_chunk<BLK, NRT>(a, lda, x, ldx, M, clen, meta, partial, blockIdx.x, As, wmax);
 }
 
+// The same 256 x 256 GEMM (tile-major rows) with two workgroups per CU: each workgroup computes half
+// the output rows (a columns 128 half .. +127: 4 row tiles x 2 column tiles per wave, 128 accumulators)
+// so the two workgroups' waves (two per SIMD) fill each other's load, split and barrier waits, which a
+// lone workgroup per CU runs in lock-step ("What bounds the phase now").  Both halves read
+// all of x: block b runs chunk (b / 16) 8 + b % 8, half (b / 8) % 2, so the halves of a chunk sit on
+// one XCD (b and b + 8) and the second read of x hits its L2.  NS raw-load sets: loads run NS - 1
+// stages ahead; the x split runs just before its stage's MFMAs (one fragment set, not two).
+template <int NS>
+__global__ void __launch_bounds__(256, 2)
+wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
+                  int clen, int chunks, H16Meta meta, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][2][128][kBfRow];   // [buffer][hi, lo][column][sample]
+  __shared__ float wmax[4][2];
+  __shared__ double bsum[128];
+  const int b = blockIdx.x;
+  const int chunk = (b >> 4) * 8 + (b & 7), half = (b >> 3) & 1;
+  if (chunk >= chunks) return;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  const int ac = 128 * half + (tid & 127), as0 = 8 * (tid >> 7);   // the thread's a column, its first sample
+  const uint32_t avo = 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0;
+  uint32_t xvo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int xc = 64 * wk + 32 * t + c;
+    xvo[t] = 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h);
+  }
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[NS][8], rx[NS][2][8];
+  double bacc = 0.0;
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, kRowLoadAux));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], j * 32, kRowLoadAux));
+  };
+  int Ea, Ex;
+  h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
+  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
+  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
+    h16x8 hi, lo;
+    split2_f16(ra[SET], sa, hi, lo);
+    *reinterpret_cast<h16x8*>(&As[buf][0][tid & 127][as0]) = hi;
+    *reinterpret_cast<h16x8*>(&As[buf][1][tid & 127][as0]) = lo;
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  constexpr int U = NS % 2 ? 2 * NS : NS;
+  const int nstages = (int)((mrel_end + U * kBfStage - 1) / (U * kBfStage)) * U;   // (extra stages add zeros)
+  load(std::integral_constant<int, 0>{}, 0);
+  if constexpr (NS > 2) load(std::integral_constant<int, (NS > 2 ? 1 : 0)>{}, 1);
+  if constexpr (NS > 3) load(std::integral_constant<int, (NS > 3 ? 2 : 0)>{}, 2);
+  split_a(std::integral_constant<int, 0>{}, 0);
+  __syncthreads();
+  // iteration st (IT = st mod U: set IT % NS, buffer IT % 2): stage st+NS-1's loads; stage st's x
+  // split and MFMAs, stage st+1's a split in their shadow; barrier
+  auto iteration = [&](auto it_c, int st) __attribute__((always_inline)) {
+    constexpr int IT = decltype(it_c)::value, SET = IT % NS, FB = IT & 1;
+    using Nxt = std::integral_constant<int, (IT + 1) % NS>;
+    using Ld = std::integral_constant<int, (IT + NS - 1) % NS>;
+    load(Ld{}, st + NS - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    h16x8 fx[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) split2_f16(rx[SET][t], sx, fx[t][0], fx[t][1]);
+    h16x8 fa[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fa[0][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][c][8 * h]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fa[(i + 1) & 1][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
+      }
+      const h16x8 (&f)[2] = fa[i & 1];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma16(f[1], fx[j][0], t);
+        t = mfma16(f[0], fx[j][1], t);
+        acc[i][j] = mfma16(f[0], fx[j][0], t);
+      }
+    }
+    split_a(Nxt{}, FB ^ 1);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);        // the x split
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);         // tile 0's reads
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+    __syncthreads();
+  };
+#define NERF_H_IT(I) \
+  if constexpr (I < U) iteration(std::integral_constant<int, (I < U ? I : 0)>{}, st + I);
+  for (int st = 0; st < nstages; st += U) {
+    NERF_H_IT(0) NERF_H_IT(1) NERF_H_IT(2) NERF_H_IT(3) NERF_H_IT(4) NERF_H_IT(5)
+  }
+#undef NERF_H_IT
+  static_assert(NS >= 2 && NS <= 3, "1..2 stages of loads in flight");
+  constexpr int KP = kWT + 1;
+  const int64_t stride = wgrad_stride(kWT, kWT);
+  float* out = partial + (size_t)chunk * stride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kk = 64 * wk + 32 * j + c;
+#pragma unroll
+      for (int g = 0; g < 16; ++g)
+        out[(size_t)(128 * half + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+    }
+  if (tid >= 128) bsum[tid - 128] = bacc;   // samples 8..15 of each stage
+  __syncthreads();
+  if (tid < 128) out[(size_t)ac * KP + kWT] = (float)(bacc + bsum[tid]);
+  if (tid == 0 && half == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
+}
+
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2831,6 +2976,18 @@ static bool wgrad_h16() {
   }();
   return on;
 }
+// The hidden layers' split-f16 GEMMs run on wgrad_h16h_kernel<3> (two workgroups per CU, half the rows
+// each); NERFMI_WGRAD_HALF=0 selects wgrad_h16w_kernel (one workgroup per CU) and =2 the two-set ring,
+// for same-process A/Bs (profiles/r05/ab_wgrad_half.log).
+static int wgrad_half() {
+  static const int ns = [] {
+    const char* e = getenv("NERFMI_WGRAD_HALF");
+    if (e && strcmp(e, "0") == 0) return 0;
+    if (e && strcmp(e, "2") == 0) return 2;
+    return 3;
+  }();
+  return ns;
+}
 
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
@@ -2865,7 +3022,13 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
       rc = check_launch("wgrad whole-tile <5>");
       scaled = h16;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
-      if (tiled)
+      if (tiled && wgrad_half() == 2)
+        hipLaunchKernelGGL(wgrad_h16h_kernel<2>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
+                           clen, chunks, hm, ws);
+      else if (tiled && wgrad_half() == 3)
+        hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
+                           clen, chunks, hm, ws);
+      else if (tiled)
         hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       else
         hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
