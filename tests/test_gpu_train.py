@@ -451,6 +451,35 @@ def test_mlp_backward_matches_autograd(ref_state, app_vec, with_app):
         no_worse_on_own_branches(grad[:, 256 * l: 256 * (l + 1)], d64_gpu[l], d32[l], d64_cpu[l], f"d pre_{l}")
 
 
+def test_weight_gradient_kernels_agree(tmp_path):
+    """The hidden layers' split-f16 weight gradients run on two workgroups per CU, half the output rows
+    each (train.hip wgrad_h16h_kernel, the default); a child process with NERFMI_WGRAD_HALF=0 runs them
+    on one workgroup per chunk (wgrad_h16w_kernel).  Same chunks, scales, fragments and MFMA order, so
+    one production-size step's weight gradients are bit-identical; the bias columns' double sums run
+    in another order (two half-stage sums), so every entry is within one float rounding."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import train_variants
+    ref = train_variants.grads()
+    out = tmp_path / "grads.pt"
+    env = dict(os.environ, NERFMI_WGRAD_HALF="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "train_variants.py"), str(out), _lib().get_mlp_arith()],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert set(got) == set(ref)
+    names = list(O.STATE_KEYS) + ["appearance_embeddings"]
+    for k in ref:
+        name = names[int(k)]
+        if name.endswith(".weight"):
+            assert torch.equal(got[k], ref[k]), name
+        else:
+            torch.testing.assert_close(got[k], ref[k], rtol=2.5e-7, atol=1e-30, msg=name)
+
+
 @pytest.mark.parametrize("R,N", [(40, 64), (2048, 64)])
 def test_param_grads_records_match_fallback(ref_state, app_vec, R, N):
     """The split-f16 weight gradient scales each chunk by its operands' largest exponents, taken from
