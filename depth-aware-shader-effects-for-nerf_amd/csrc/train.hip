@@ -2446,10 +2446,12 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
 // all of x: block b runs chunk (b / 16) 8 + b % 8, half (b / 8) % 2, so the halves of a chunk sit on
 // one XCD (b and b + 8) and the second read of x hits its L2.  NS raw-load sets: loads run NS - 1
 // stages ahead; the x split runs just before its stage's MFMAs (one fragment set, not two).
+// nrows < 256 (the dir/density launch: 160): a columns from nrows on are not read (zeros) and
+// output rows from nrows on are not stored; the partial has nrows rows (wgrad_stride(nrows, 256)).
 template <int NS>
 __global__ void __launch_bounds__(256, 2)
 wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                  int clen, int chunks, H16Meta meta, float* __restrict__ partial) {
+                  int clen, int chunks, int nrows, H16Meta meta, float* __restrict__ partial) {
   __shared__ __attribute__((aligned(16))) _Float16 As[2][2][128][kBfRow];   // [buffer][hi, lo][column][sample]
   __shared__ float wmax[4][2];
   __shared__ double bsum[128];
@@ -2462,7 +2464,7 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   const int h = lane >> 5, c = lane & 31;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
   const int ac = 128 * half + (tid & 127), as0 = 8 * (tid >> 7);   // the thread's a column, its first sample
-  const uint32_t avo = 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0;
+  const uint32_t avo = ac < nrows ? 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0 : 0x80000000u;
   uint32_t xvo[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -2567,20 +2569,23 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
 #undef NERF_H_IT
   static_assert(NS >= 2 && NS <= 3, "1..2 stages of loads in flight");
   constexpr int KP = kWT + 1;
-  const int64_t stride = wgrad_stride(kWT, kWT);
+  const int64_t stride = wgrad_stride(nrows, kWT);
   float* out = partial + (size_t)chunk * stride;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    if (128 * half + 32 * i < nrows) {   // (uniform: whole row tiles past the kept rows are dropped)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
+      for (int j = 0; j < 2; ++j) {
+        const int kk = 64 * wk + 32 * j + c;
 #pragma unroll
-      for (int g = 0; g < 16; ++g)
-        out[(size_t)(128 * half + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+        for (int g = 0; g < 16; ++g)
+          out[(size_t)(128 * half + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+      }
     }
+  }
   if (tid >= 128) bsum[tid - 128] = bacc;   // samples 8..15 of each stage
   __syncthreads();
-  if (tid < 128) out[(size_t)ac * KP + kWT] = (float)(bacc + bsum[tid]);
+  if (tid < 128 && ac < nrows) out[(size_t)ac * KP + kWT] = (float)(bacc + bsum[tid]);
   if (tid == 0 && half == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
 }
 
@@ -2976,9 +2981,10 @@ static bool wgrad_h16() {
   }();
   return on;
 }
-// The hidden layers' split-f16 GEMMs run on wgrad_h16h_kernel<3> (two workgroups per CU, half the rows
-// each); NERFMI_WGRAD_HALF=0 selects wgrad_h16w_kernel (one workgroup per CU) and =2 the two-set ring,
-// for same-process A/Bs (profiles/r05/ab_wgrad_half.log).
+// The hidden layers' and the dir/density launch's split-f16 GEMMs run on wgrad_h16h_kernel<3> (two
+// workgroups per CU, half the rows each); NERFMI_WGRAD_HALF=0 selects wgrad_h16w_kernel (one workgroup
+// per CU) for both and =2 the two-set ring, for same-process A/Bs (profiles/r05/ab_wgrad_half.log,
+// ab_wgrad_dir.log).
 static int wgrad_half() {
   static const int ns = [] {
     const char* e = getenv("NERFMI_WGRAD_HALF");
@@ -3013,7 +3019,10 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     chunks = (int)((M + clen - 1) / clen);
     const bool h16 = wgrad_h16();
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      if (h16)
+      if (h16 && wgrad_half() == 3)   // two workgroups per CU, 160 of 256 rows kept
+        hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
+                           clen, chunks, N, hm, ws);
+      else if (h16)
         hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                            hm, ws);
       else
@@ -3024,10 +3033,10 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
       if (tiled && wgrad_half() == 2)
         hipLaunchKernelGGL(wgrad_h16h_kernel<2>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, hm, ws);
+                           clen, chunks, kWT, hm, ws);
       else if (tiled && wgrad_half() == 3)
         hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, hm, ws);
+                           clen, chunks, kWT, hm, ws);
       else if (tiled)
         hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       else
