@@ -2439,6 +2439,156 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   h16w_chunk<BLK, NRT>(a, lda, x, ldx, M, clen, meta, partial, blockIdx.x, As, wmax);
 }
 
+// The same 256 x 256 GEMM (tile-major rows) with two workgroups per CU: each workgroup computes half
+// the output rows (a columns 128 half .. +127: 4 row tiles x 2 column tiles per wave, 128 accumulators)
+// so the two workgroups' waves (two per SIMD) fill each other's load, split and barrier waits, which a
+// lone workgroup per CU runs in lock-step (DESIGN §8, "What bounds the phase now").  Both halves read
+// all of x: block b runs chunk (b / 16) 8 + b % 8, half (b / 8) % 2, so the halves of a chunk sit on
+// one XCD (b and b + 8) and the second read of x hits its L2.  NS raw-load sets: loads run NS - 1
+// stages ahead; the x split runs just before its stage's MFMAs (one fragment set, not two).
+// nrows < 256 (the dir/density launch: 160): a columns from nrows on are not read (zeros) and
+// output rows from nrows on are not stored; the partial has nrows rows (wgrad_stride(nrows, 256)).
+template <int NS>
+__global__ void __launch_bounds__(256, 2)
+wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
+                  int clen, int chunks, int nrows, H16Meta meta, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][2][128][kBfRow];   // [buffer][hi, lo][column][sample]
+  __shared__ float wmax[4][2];
+  __shared__ double bsum[128];
+  const int b = blockIdx.x;
+  const int chunk = (b >> 4) * 8 + (b & 7), half = (b >> 3) & 1;
+  if (chunk >= chunks) return;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
+  const int ac = 128 * half + (tid & 127), as0 = 8 * (tid >> 7);   // the thread's a column, its first sample
+  const uint32_t avo = ac < nrows ? 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0 : 0x80000000u;
+  uint32_t xvo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int xc = 64 * wk + 32 * t + c;
+    xvo[t] = 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h);
+  }
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+  float ra[NS][8], rx[NS][2][8];
+  double bacc = 0.0;
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, kRowLoadAux));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], j * 32, kRowLoadAux));
+  };
+  int Ea, Ex;
+  h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
+  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
+  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
+    h16x8 hi, lo;
+    split2_f16(ra[SET], sa, hi, lo);
+    *reinterpret_cast<h16x8*>(&As[buf][0][tid & 127][as0]) = hi;
+    *reinterpret_cast<h16x8*>(&As[buf][1][tid & 127][as0]) = lo;
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  constexpr int U = NS % 2 ? 2 * NS : NS;
+  const int nstages = (int)((mrel_end + U * kBfStage - 1) / (U * kBfStage)) * U;   // (extra stages add zeros)
+  load(std::integral_constant<int, 0>{}, 0);
+  if constexpr (NS > 2) load(std::integral_constant<int, (NS > 2 ? 1 : 0)>{}, 1);
+  if constexpr (NS > 3) load(std::integral_constant<int, (NS > 3 ? 2 : 0)>{}, 2);
+  split_a(std::integral_constant<int, 0>{}, 0);
+  __syncthreads();
+  // iteration st (IT = st mod U: set IT % NS, buffer IT % 2): stage st+NS-1's loads; stage st's x
+  // split and MFMAs, stage st+1's a split in their shadow; barrier
+  auto iteration = [&](auto it_c, int st) __attribute__((always_inline)) {
+    constexpr int IT = decltype(it_c)::value, SET = IT % NS, FB = IT & 1;
+    using Nxt = std::integral_constant<int, (IT + 1) % NS>;
+    using Ld = std::integral_constant<int, (IT + NS - 1) % NS>;
+    load(Ld{}, st + NS - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    h16x8 fx[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) split2_f16(rx[SET][t], sx, fx[t][0], fx[t][1]);
+    h16x8 fa[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fa[0][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][c][8 * h]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fa[(i + 1) & 1][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
+      }
+      const h16x8 (&f)[2] = fa[i & 1];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 t = acc[i][j];
+        t = mfma16(f[1], fx[j][0], t);
+        t = mfma16(f[0], fx[j][1], t);
+        acc[i][j] = mfma16(f[0], fx[j][0], t);
+      }
+    }
+    split_a(Nxt{}, FB ^ 1);
+    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);        // the x split
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);         // tile 0's reads
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+    __syncthreads();
+  };
+#define NERF_H_IT(I) \
+  if constexpr (I < U) iteration(std::integral_constant<int, (I < U ? I : 0)>{}, st + I);
+  for (int st = 0; st < nstages; st += U) {
+    NERF_H_IT(0) NERF_H_IT(1) NERF_H_IT(2) NERF_H_IT(3) NERF_H_IT(4) NERF_H_IT(5)
+  }
+#undef NERF_H_IT
+  static_assert(NS >= 2 && NS <= 3, "1..2 stages of loads in flight");
+  constexpr int KP = kWT + 1;
+  const int64_t stride = wgrad_stride(nrows, kWT);
+  float* out = partial + (size_t)chunk * stride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (128 * half + 32 * i < nrows) {   // (uniform: whole row tiles past the kept rows are dropped)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int kk = 64 * wk + 32 * j + c;
+#pragma unroll
+        for (int g = 0; g < 16; ++g)
+          out[(size_t)(128 * half + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
+      }
+    }
+  }
+  if (tid >= 128) bsum[tid - 128] = bacc;   // samples 8..15 of each stage
+  __syncthreads();
+  if (tid < 128 && ac < nrows) out[(size_t)ac * KP + kWT] = (float)(bacc + bsum[tid]);
+  if (tid == 0 && half == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
+}
+
 // 256 x (K <= 64) weight gradients with one x row per sample (layer 0 and the skip layer's PE
 // columns): 8 waves, wave w owns output rows 32w .. 32w+31 (one MFMA row tile, two column tiles).
 // Each wave loads its own a columns straight in A-fragment order (lane (c, h): column 32w + c,
@@ -2683,7 +2833,7 @@ struct WgradSplit {                  // rows n0 <= n < n_end of a weight gradien
 constexpr int kRedParts = NERF_RED_PARTS;
 __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ partial, int chunks, int N, int K,
                                                   float* __restrict__ out_w, int ldo, float* __restrict__ out_b,
-                                                  int accumulate, const WgradSplit& split, int scaled, int rb) {
+                                                  int accumulate, const WgradSplit& split, int scaled) {
   // the chunk partials are added in double and rounded once: a gradient entry is a sum over up to
   // 2^18 samples with heavy cancellation (random-sign upstream gradients), and an fp32 running sum of
   // its 256 chunk partials cost up to ~10x the fp32 CPU autograd's error on the bias columns
@@ -2692,7 +2842,7 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
   __shared__ f64x4 part[kRedParts][64];
   const int KP = K + 1;
   const int64_t stride = wgrad_stride(N, K);
-  const int64_t col4 = (int64_t)rb * 64 + (threadIdx.x & 63);
+  const int64_t col4 = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int q = threadIdx.x >> 6;
   const int per = (chunks + kRedParts - 1) / kRedParts;
   const int c0 = q * per < chunks ? q * per : chunks, c1 = c0 + per < chunks ? c0 + per : chunks;
@@ -2743,7 +2893,7 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
   }
   part[q][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (q != 0 || col4 * 4 >= stride) return;   // (no barrier follows: callers looping over rb sync first)
+  if (q != 0 || col4 * 4 >= stride) return;
   f64x4 sum64 = part[0][threadIdx.x];
 #pragma unroll
   for (int r = 1; r < kRedParts; ++r) sum64 += part[r][threadIdx.x];
@@ -2769,182 +2919,8 @@ __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ part
 __global__ void __launch_bounds__(64 * kRedParts)
 wgrad_reduce_kernel(const float* __restrict__ partial, int chunks, int N, int K, float* __restrict__ out_w, int ldo,
                     float* __restrict__ out_b, int accumulate, WgradSplit split, int scaled) {
-  wgrad_reduce_body(partial, chunks, N, K, out_w, ldo, out_b, accumulate, split, scaled, blockIdx.x);
+  wgrad_reduce_body(partial, chunks, N, K, out_w, ldo, out_b, accumulate, split, scaled);
 }
-
-// A chunk reduction's arguments (wgrad_reduce_kernel / wgrad_reduce_body), to run later (RedJob chain).
-struct RedJob {
-  const float* partial = nullptr;
-  int chunks = 0, N = 0, K = 0;
-  float* out_w = nullptr;
-  int ldo = 0;
-  float* out_b = nullptr;
-  WgradSplit split{};
-  int scaled = 0;
-};
-
-// The same 256 x 256 GEMM (tile-major rows) with two workgroups per CU: each workgroup computes half
-// the output rows (a columns 128 half .. +127: 4 row tiles x 2 column tiles per wave, 128 accumulators)
-// so the two workgroups' waves (two per SIMD) fill each other's load, split and barrier waits, which a
-// lone workgroup per CU runs in lock-step (DESIGN §8, "What bounds the phase now").  Both halves read
-// all of x: block b runs chunk (b / 16) 8 + b % 8, half (b / 8) % 2, so the halves of a chunk sit on
-// one XCD (b and b + 8) and the second read of x hits its L2.  NS raw-load sets: loads run NS - 1
-// stages ahead; the x split runs just before its stage's MFMAs (one fragment set, not two).
-// nrows < 256 (the dir/density launch: 160): a columns from nrows on are not read (zeros) and
-// output rows from nrows on are not stored; the partial has nrows rows (wgrad_stride(nrows, 256)).
-// prev (partial non-null): the chunk reduction of the previous weight-gradient launch on this stream,
-// run by this launch's workgroups after their own chunk (workgroup 2 chunk + half takes reduction
-// blocks idx, idx + 2 chunks, ...; each block sums its columns over the chunks in fixed order, as
-// wgrad_reduce_kernel): no separate reduction launch between the GEMM launches of a stream.
-template <int NS>
-__global__ void __launch_bounds__(256, 2)
-wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                  int clen, int chunks, int nrows, H16Meta meta, float* __restrict__ partial, RedJob prev) {
-  __shared__ __attribute__((aligned(16))) _Float16 As[2][2][128][kBfRow];   // [buffer][hi, lo][column][sample]
-  __shared__ float wmax[4][2];
-  __shared__ double bsum[128];
-  const int b = blockIdx.x;
-  const int chunk = (b >> 4) * 8 + (b & 7), half = (b >> 3) & 1;
-  if (chunk >= chunks) return;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;
-  const int h = lane >> 5, c = lane & 31;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const int ac = 128 * half + (tid & 127), as0 = 8 * (tid >> 7);   // the thread's a column, its first sample
-  const uint32_t avo = ac < nrows ? 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0 : 0x80000000u;
-  uint32_t xvo[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int xc = 64 * wk + 32 * t + c;
-    xvo[t] = 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h);
-  }
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[NS][8], rx[NS][2][8];
-  double bacc = 0.0;
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a + (ms / 32) * 32 * lda + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + (ms / 32) * 32 * ldx + (ms % 32) * 8), (short)0,
-        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, kRowLoadAux));
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], j * 32, kRowLoadAux));
-  };
-  int Ea, Ex;
-  h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
-  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
-  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
-    h16x8 hi, lo;
-    split2_f16(ra[SET], sa, hi, lo);
-    *reinterpret_cast<h16x8*>(&As[buf][0][tid & 127][as0]) = hi;
-    *reinterpret_cast<h16x8*>(&As[buf][1][tid & 127][as0]) = lo;
-  };
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  constexpr int U = NS % 2 ? 2 * NS : NS;
-  const int nstages = (int)((mrel_end + U * kBfStage - 1) / (U * kBfStage)) * U;   // (extra stages add zeros)
-  load(std::integral_constant<int, 0>{}, 0);
-  if constexpr (NS > 2) load(std::integral_constant<int, (NS > 2 ? 1 : 0)>{}, 1);
-  if constexpr (NS > 3) load(std::integral_constant<int, (NS > 3 ? 2 : 0)>{}, 2);
-  split_a(std::integral_constant<int, 0>{}, 0);
-  __syncthreads();
-  // iteration st (IT = st mod U: set IT % NS, buffer IT % 2): stage st+NS-1's loads; stage st's x
-  // split and MFMAs, stage st+1's a split in their shadow; barrier
-  auto iteration = [&](auto it_c, int st) __attribute__((always_inline)) {
-    constexpr int IT = decltype(it_c)::value, SET = IT % NS, FB = IT & 1;
-    using Nxt = std::integral_constant<int, (IT + 1) % NS>;
-    using Ld = std::integral_constant<int, (IT + NS - 1) % NS>;
-    load(Ld{}, st + NS - 1);
-    __builtin_amdgcn_sched_barrier(0);
-    h16x8 fx[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) split2_f16(rx[SET][t], sx, fx[t][0], fx[t][1]);
-    h16x8 fa[2][2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) fa[0][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][c][8 * h]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i + 1 < 4) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          fa[(i + 1) & 1][p] = *reinterpret_cast<const h16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
-      }
-      const h16x8 (&f)[2] = fa[i & 1];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma16(f[1], fx[j][0], t);
-        t = mfma16(f[0], fx[j][1], t);
-        acc[i][j] = mfma16(f[0], fx[j][0], t);
-      }
-    }
-    split_a(Nxt{}, FB ^ 1);
-    __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);        // the x split
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);         // tile 0's reads
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-    __syncthreads();
-  };
-#define NERF_H_IT(I) \
-  if constexpr (I < U) iteration(std::integral_constant<int, (I < U ? I : 0)>{}, st + I);
-  for (int st = 0; st < nstages; st += U) {
-    NERF_H_IT(0) NERF_H_IT(1) NERF_H_IT(2) NERF_H_IT(3) NERF_H_IT(4) NERF_H_IT(5)
-  }
-#undef NERF_H_IT
-  static_assert(NS >= 2 && NS <= 3, "1..2 stages of loads in flight");
-  constexpr int KP = kWT + 1;
-  const int64_t stride = wgrad_stride(nrows, kWT);
-  float* out = partial + (size_t)chunk * stride;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (128 * half + 32 * i < nrows) {   // (uniform: whole row tiles past the kept rows are dropped)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-        for (int g = 0; g < 16; ++g)
-          out[(size_t)(128 * half + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-      }
-    }
-  }
-  if (tid >= 128) bsum[tid - 128] = bacc;   // samples 8..15 of each stage
-  __syncthreads();
-  if (tid < 128 && ac < nrows) out[(size_t)ac * KP + kWT] = (float)(bacc + bsum[tid]);
-  if (tid == 0 && half == 0) reinterpret_cast<int*>(out)[stride - 4] = Ea + Ex - 28;
-  if (prev.partial) {
-    const int nrb = (int)((wgrad_stride(prev.N, prev.K) / 4 + 63) / 64);
-    for (int rb = 2 * chunk + half; rb < nrb; rb += 2 * chunks) {   // (uniform per workgroup)
-      __syncthreads();
-      wgrad_reduce_body(prev.partial, prev.chunks, prev.N, prev.K, prev.out_w, prev.ldo, prev.out_b, 0, prev.split,
-                        prev.scaled, rb);
-    }
-  }
-}
-
 
 size_t wgrad_workspace_floats(int64_t M, int N, int K) {
   const int clen = wgrad_chunk_len(N, K, M);   // >= the chunk count of every path of launch_wgrad
@@ -3009,14 +2985,6 @@ static bool wgrad_h16() {
 // workgroups per CU, half the rows each); NERFMI_WGRAD_HALF=0 selects wgrad_h16w_kernel (one workgroup
 // per CU) for both and =2 the two-set ring, for same-process A/Bs (profiles/r05/ab_wgrad_half.log,
 // ab_wgrad_dir.log).
-// NERFMI_WGRAD_CHAIN=0: every weight-gradient launch runs its own reduction launch (A/B)
-static bool wgrad_chain() {
-  static const bool on = [] {
-    const char* e = getenv("NERFMI_WGRAD_CHAIN");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  return on;
-}
 static int wgrad_half() {
   static const int ns = [] {
     const char* e = getenv("NERFMI_WGRAD_HALF");
@@ -3031,34 +2999,12 @@ static int wgrad_half() {
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
 // appearance projection's x (the embedding rows, one per ray) is row-major: x_tiled = false.
 // meta: the block exponents of a and x (layout.h) for the split-f16 whole-tile kernel (nullable).
-// The pending chunk reduction of a stream's previous launch (RedJob chain): launched on its own.
-static int flush_red(RedJob* chain, hipStream_t s) {
-  if (!chain || !chain->partial) return NERF_OK;
-  const RedJob r = *chain;
-  chain->partial = nullptr;
-  const int64_t cols4 = wgrad_stride(r.N, r.K) / 4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, r.partial,
-                     r.chunks, r.N, r.K, r.out_w, r.ldo, r.out_b, 0, r.split, r.scaled);
-  return check_launch("wgrad_reduce_kernel");
-}
-
-// chain (nullable): the stream's pending reduction.  A launch on wgrad_h16h_kernel runs the pending
-// reduction inside its workgroups and leaves its own pending in *chain (the caller gives it a partial
-// buffer other than the pending one's); any other launch flushes the pending reduction first.
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
                  const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true,
-                 const H16Meta* meta = nullptr, RedJob* chain = nullptr) {
+                 const H16Meta* meta = nullptr) {
   const H16Meta hm = meta ? *meta : H16Meta{};
   if (M == 0) return NERF_OK;
-  // (a chained reduction writes, never accumulates; and a launch must not overwrite the partial the
-  // pending reduction reads: run the pending one first then)
-  if (chain && (accumulate != 0 || chain->partial == ws)) {
-    if (int rc0 = flush_red(chain, s)) return rc0;
-  }
-  const bool chainable = chain && accumulate == 0;
-  const RedJob prev = chainable ? *chain : RedJob{};
-  bool half_launched = false;                           // (wgrad_h16h_kernel ran the pending reduction)
   const int KP = K + 1;
   int chunks = (int)((M + kWChunk - 1) / kWChunk);
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)x % 16 == 0) && lda % 4 == 0 && ldx % 4 == 0;
@@ -3073,11 +3019,10 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     chunks = (int)((M + clen - 1) / clen);
     const bool h16 = wgrad_h16();
     if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      if (h16 && wgrad_half() == 3) {   // two workgroups per CU, 160 of 256 rows kept
+      if (h16 && wgrad_half() == 3)   // two workgroups per CU, 160 of 256 rows kept
         hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, N, hm, ws, prev);
-        half_launched = true;
-      } else if (h16)
+                           clen, chunks, N, hm, ws);
+      else if (h16)
         hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
                            hm, ws);
       else
@@ -3086,15 +3031,13 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
       rc = check_launch("wgrad whole-tile <5>");
       scaled = h16;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
-      if (tiled && wgrad_half() == 2) {
+      if (tiled && wgrad_half() == 2)
         hipLaunchKernelGGL(wgrad_h16h_kernel<2>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, kWT, hm, ws, prev);
-        half_launched = true;
-      } else if (tiled && wgrad_half() == 3) {
+                           clen, chunks, kWT, hm, ws);
+      else if (tiled && wgrad_half() == 3)
         hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, kWT, hm, ws, prev);
-        half_launched = true;
-      } else if (tiled)
+                           clen, chunks, kWT, hm, ws);
+      else if (tiled)
         hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       else
         hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
@@ -3147,11 +3090,6 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     rc = check_launch("wgrad_kernel");
   }
   if (rc) return rc;
-  if (half_launched && chainable) {   // the kernel ran the pending reduction; its own runs later
-    *chain = RedJob{ws, chunks, N, K, out_w, ldo, out_b, split ? *split : WgradSplit{}, (int)scaled};
-    return NERF_OK;
-  }
-  if ((rc = flush_red(chain, s))) return rc;   // (another kernel: the pending reduction on its own)
   const int64_t cols4 = wgrad_stride(N, K) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks, N, K,
                      out_w, ldo, out_b, accumulate, split ? *split : WgradSplit{}, (int)scaled);
@@ -3282,10 +3220,9 @@ static size_t wgrad_stream_floats(int64_t M) {
   }
   return m;
 }
-// param_grads' workspace: two partial buffers for each of the two streams (chained reductions) + the
-// ray-sum buffers
+// param_grads' workspace: two streams' partial buffers + the ray-sum buffers
 static size_t max_wgrad_floats(int64_t M) {
-  return 4 * ((wgrad_stream_floats(M) + 63) & ~(size_t)63) + ray_sum_floats(M) + 64;
+  return 2 * ((wgrad_stream_floats(M) + 63) & ~(size_t)63) + ray_sum_floats(M) + 64;
 }
 
 // Which MLP arithmetic the last nerf_train_forward on a workspace ran under (the f32 forward writes no
@@ -3451,15 +3388,9 @@ static H16Meta block_exps(const float* save, const float* grad, int ja, int jx) 
 
 // The jobs, on streams sa / sb with partial buffers wa / wb (wfl floats each) and the ray-sum
 // buffers at `rays` (N >= kRaySumMinN).
-// Chained (ca, cb non-null): each stream owns two partial buffers (wa / wa2, wb / wb2) and a pending
-// reduction (RedJob chain): a launch writes the buffer its stream's pending reduction does not read.
 static int param_grads_jobs(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
                             const float* packed, float* const* g, float* dapp, float* wa, float* wb, size_t wfl,
-                            float* rays, hipStream_t sa, hipStream_t sb, RedJob* ca = nullptr, RedJob* cb = nullptr,
-                            float* wa2 = nullptr, float* wb2 = nullptr) {
-  // the buffer of the next launch on stream A (B): the one the stream's pending reduction does not read
-  auto buf_a = [&]() { return ca && ca->partial == wa ? wa2 : wa; };
-  auto buf_b = [&]() { return cb && cb->partial == wb ? wb2 : wb; };
+                            float* rays, hipStream_t sa, hipStream_t sb) {
   // Job: columns [k0, k0 + K) of parameter p's weight gradient (row length ldo) from x; the bias
   // gradient with the first column block only.  The skip layer's [h3 | enc_x] runs as a 256 x 256
   // block (the whole-tile kernel) plus the 63 PE columns, instead of one 256 x 319 GEMM on 128 x 128
@@ -3484,7 +3415,7 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
 #ifndef NERF_PE_SEPARATE   // (A/B build: layer 0 and the skip PE columns as two K = 63 launches)
-  if ((rc = flush_red(cb, sb)) || (rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], buf_b(), wfl, sb))) return rc;
+  if ((rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
 #endif
   for (const Job& j : jobs) {
 #ifndef NERF_PE_SEPARATE
@@ -3493,17 +3424,16 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
 #ifndef NERF_HEAD3_GEMM   // (A/B build: the rgb head on the 128 x 128 tile GEMM)
     if (j.a == kGradRgb) {   // the rgb head: the streaming kernel (3 rows)
-      if ((rc = flush_red(j.b ? cb : ca, j.b ? sb : sa)) ||
-          (rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
-                                   j.b ? buf_b() : buf_a(), wfl, j.b ? sb : sa)))
+      if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
+                                   j.b ? wb : wa, wfl, j.b ? sb : sa)))
         return rc;
       continue;
     }
 #endif
     const H16Meta hm = block_exps(save, grad, j.ja, j.jx);
     if ((rc = launch_wgrad(grad + tile_col(j.a), kGradRow, j.n, save + tile_col(j.x), kSaveRow, j.K, 1, M, g[j.p] + j.k0,
-                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? buf_b() : buf_a(), j.b ? sb : sa, nullptr, true,
-                           true, j.ja >= 0 ? &hm : nullptr, j.b ? cb : ca)))
+                           j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? wb : wa, j.b ? sb : sa, nullptr, true, true,
+                           j.ja >= 0 ? &hm : nullptr)))
       return rc;
   }
   static_assert(kGradSigma == kGradDir + kDirHidden, "the density head's gradient follows dir_linear's");
@@ -3523,16 +3453,16 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     H16Meta hm = block_exps(save, grad, 7, 7);
     hm.a_cols = kDirHidden + 1;                            // d pre_dir, d sigma (rows 129.. are dropped)
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
-                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, buf_b(), sb, &heads, true, true, &hm, cb)))
+                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm)))
       return rc;
     hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, sb, grad, save, N, S, E);
     if ((rc = check_launch("ray_sums_kernel"))) return rc;
     if ((rc = launch_wgrad(S, 256, kDirHidden, E, 32, kDirEnc, 1, B, g[P_DIR_W] + kHidden, kHidden + kDirEnc, nullptr,
-                           0, buf_b(), sb, nullptr, false, true, nullptr, cb)))
+                           0, wb, sb)))
       return rc;
     if (app_rows == 0) return NERF_OK;     // no appearance: the projection is unused (models.py:146)
     if ((rc = launch_wgrad(S + kDirHidden, 256, kDirHidden, app, kAppDim, kAppDim, app_rows == 1 ? 0 : 1, B,
-                           g[P_APP_W], kAppDim, g[P_APP_B], 0, buf_b(), sb, nullptr, false, true, nullptr, cb)))
+                           g[P_APP_W], kAppDim, g[P_APP_B], 0, wb, sb)))
       return rc;
     if (!dapp) return NERF_OK;
     if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, sb, false);
@@ -3545,8 +3475,7 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
   const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B]};
   if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirHidden + 1, save + tile_col(save_h(7)), kSaveRow,
-                         kHidden + kDirEnc, 1, M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, buf_b(), sb, &heads, true,
-                         true, nullptr, cb)))
+                         kHidden + kDirEnc, 1, M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true)))
     return rc;
   if (app_rows == 0) {   // no appearance: the projection is unused (models.py:146)
     return NERF_OK;
@@ -3554,7 +3483,7 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   // appearance_projection: x = the ray's embedding row (broadcast when app_rows == 1; row-major)
   const int64_t xdiv = app_rows == 1 ? 0 : N;
   if ((rc = launch_wgrad(grad + tile_col(kGradHd), kGradRow, kDirHidden, app, kAppDim, kAppDim, xdiv, M, g[P_APP_W],
-                         kAppDim, g[P_APP_B], 0, buf_b(), sb, nullptr, true, /*x_tiled=*/false, nullptr, cb)))
+                         kAppDim, g[P_APP_B], 0, wb, sb, nullptr, true, /*x_tiled=*/false)))
     return rc;
   if (!dapp) return NERF_OK;
   if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, sb, false);
@@ -3585,17 +3514,7 @@ static int param_grads(const float* save, const float* grad, int64_t M, int N, c
   if ((rc = pg_streams(&ps))) return rc;
   if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->s2, ps->fork, 0) != hipSuccess)
     return set_error(NERF_ERR_HIP, "param_grads: stream fork failed");
-  // chained reductions (wgrad_h16h_kernel runs its stream's previous reduction): two partial buffers
-  // per stream when the workspace holds them (nerf_param_grads_workspace_bytes does)
-  const bool chained = avail >= 4 * w1 && wgrad_chain();
-  RedJob ca, cb;
-  rc = chained ? param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2, &ca,
-                                  &cb, ws + 2 * w1, ws + 3 * w1)
-               : param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2);
-  if (chained) {   // the streams' last reductions (also after a failure: queued kernels still read them)
-    const int r1 = flush_red(&ca, s), r2 = flush_red(&cb, ps->s2);
-    rc = rc ? rc : (r1 ? r1 : r2);
-  }
+  rc = param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws + w1, w1, rays, s, ps->s2);
   // join even after a failed launch, so the caller's stream never runs ahead of queued work
   if (hipEventRecord(ps->join, ps->s2) != hipSuccess || hipStreamWaitEvent(s, ps->join, 0) != hipSuccess)
     return rc ? rc : set_error(NERF_ERR_HIP, "param_grads: stream join failed");
