@@ -510,13 +510,15 @@ def test_param_grads_records_match_fallback(ref_state, app_vec, R, N):
         assert torch.isfinite(g1).all(), k
 
 
-@pytest.mark.parametrize("with_app", [False, True])
-def test_param_grads_match_autograd(ref_state, app_vec, with_app):
-    """nerf_param_grads (every weight gradient as an MFMA reduction) on the chain above."""
+@pytest.mark.parametrize("with_app,R", [(False, 96), (True, 96), (True, 37)])
+def test_param_grads_match_autograd(ref_state, app_vec, with_app, R):
+    """nerf_param_grads (every weight gradient as an MFMA reduction) on the chain above.  R = 37: 407
+    samples, so the whole-tile GEMMs run 26 chunks of 16 with a 7-sample last chunk, and the grid of
+    the two-workgroups-per-CU kernel (rounded up to 8 chunks) has idle workgroups."""
     L = _lib()
     lib, dev = L.load(), L.device()
     app = app_vec if with_app else None
-    R, N = 96, 11
+    N = 11
     r = _mlp_forward_backward(ref_state, app, R=R, N=N)
     save, grad = r["save_tiled"].to(dev), r["grad_tiled"].to(dev)
     packed, _, ts = packed_of(ref_state, dev)
