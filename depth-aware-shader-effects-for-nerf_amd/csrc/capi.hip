@@ -123,10 +123,16 @@ NERF_HD inline uint32_t pack16_word(const float* const* P, const float* consts, 
 
 struct ParamPtrs { const float* p[P_COUNT]; };
 
+// (the last block also zeroes the split stream's constant slots, which scale16_kernel's atomics fill)
 __global__ void __launch_bounds__(256) pack_kernel(ParamPtrs P, float* __restrict__ packed) {
+  if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < kS16Consts) packed[kOffScale16 + threadIdx.x] = 0.0f;
+    return;
+  }
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < kOff16) packed[e] = e < kF32Floats ? pack_value(P.p, e) : 0.0f;
 }
+static_assert(kS16Consts <= 256, "one block zeroes the constant slots");
 
 // One block per layer: its scale, bound constants (layout.h).
 // Layer statistics for the split scales: each wave reduces 8 rows (lanes over the row's columns,
@@ -140,19 +146,31 @@ constexpr int kS16RowsPerWave = 8;
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
   __shared__ float red[3][4];
   const int L = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the wave's 8 rows loaded first (one memory round trip, not one per row), then per row the lane's
+  // column-order sum and the xor tree as before (zeros past a row's end add nothing)
+  const int rows = layer_rows(L), cols = layer_cols(L);
+  constexpr int kColSteps = (kHidden + kPosEnc + 63) / 64;
+  float w[kS16RowsPerWave][kColSteps];
+#pragma unroll
+  for (int j = 0; j < kS16RowsPerWave; ++j)
+#pragma unroll
+    for (int q = 0; q < kColSteps; ++q) {
+      const int row = (blockIdx.x * 4 + wave) * kS16RowsPerWave + j, c = lane + 64 * q;
+      w[j][q] = row < rows && c < cols ? fabsf(layer_weight(P.p, L, row, c)) : 0.0f;
+    }
   float mx = 0.0f, l1m = 0.0f, bm = 0.0f;
+#pragma unroll
   for (int j = 0; j < kS16RowsPerWave; ++j) {
     const int row = (blockIdx.x * 4 + wave) * kS16RowsPerWave + j;
-    if (row >= layer_rows(L)) break;
     float l1 = 0.0f;
-    for (int c = lane; c < layer_cols(L); c += 64) {
-      const float w = fabsf(layer_weight(P.p, L, row, c));
-      mx = fmaxf(mx, w);
-      l1 += w;
+#pragma unroll
+    for (int q = 0; q < kColSteps; ++q) {
+      mx = fmaxf(mx, w[j][q]);
+      l1 += w[j][q];
     }
     for (int off = 32; off > 0; off >>= 1) l1 += __shfl_xor(l1, off);
     l1m = fmaxf(l1m, l1);
-    if (L < 8) bm = fmaxf(bm, fabsf(P.p[2 * L + 1][row]));
+    if (L < 8 && row < rows) bm = fmaxf(bm, fabsf(P.p[2 * L + 1][row]));
   }
   for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   if (lane == 0) {
@@ -194,10 +212,8 @@ __global__ void __launch_bounds__(256) pack16_kernel(ParamPtrs P, float* __restr
 int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   ParamPtrs P;
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kOff16 + 255) / 256)), dim3(256), 0, s, P, packed);
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((kOff16 + 255) / 256 + 1)), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("pack_kernel")) return rc;
-  if (hipMemsetAsync(packed + kOffScale16, 0, kS16Consts * sizeof(float), s) != hipSuccess)
-    return set_error(NERF_ERR_HIP, "pack: hipMemsetAsync failed");
   hipLaunchKernelGGL(scale16_kernel, dim3(kHidden / (4 * kS16RowsPerWave), kS16Layers), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("scale16_kernel")) return rc;
   hipLaunchKernelGGL(scale16_finalize_kernel, dim3(1), dim3(64), 0, s, packed);
