@@ -560,11 +560,11 @@ static int render_rays_chunk(const float* packed, const float* rays_o, const flo
   const uint64_t seed_c = rng_key_at(seed, (uint64_t)ray0 * (uint64_t)N);
   const uint64_t seed_f = rng_key_at(seed ^ 0x5DEECE66Dull, (uint64_t)ray0 * (uint64_t)Nf);
   int rc;
-  if ((rc = launch_normalize(rays_d, B, dn, s))) return rc;                                   // render.py:19
+  // render.py:19's normalisation in the ray-feature kernel (it writes dn)
+  if ((rc = launch_ray_features(packed, rays_d, B, app, app_rows, feat, s, nullptr, dn))) return rc;
   if ((rc = launch_stratified(rays_o, dn, B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand, seed_c,
                               z, nullptr, s)))
     return rc;                                                                                 // render.py:22
-  if ((rc = launch_ray_features(packed, dn, B, app, app_rows, feat, s))) return rc;
   if ((rc = profiled_mlp(packed, rays_o, dn, z, B, N, feat, rgb_c, sigma_c, nullptr, 0, s))) return rc;  // :49
   if (Nf == 0)
     return launch_composite(rgb_c, sigma_c, z, B, N, rgb_map, depth_map, wc, s);               // render.py:56-80

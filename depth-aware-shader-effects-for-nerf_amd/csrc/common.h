@@ -139,7 +139,7 @@ int launch_importance(const float* o, const float* d, const float* z, const floa
                       uint16_t* merged_src = nullptr);
 int launch_pack(const float* const* params, float* packed, hipStream_t s);
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
-                        int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr);
+                        int64_t app_rows, float* feat, hipStream_t s, float* encd = nullptr, float* dn_out = nullptr);
 extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,

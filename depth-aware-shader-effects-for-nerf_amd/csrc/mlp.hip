@@ -374,27 +374,48 @@ constexpr int kFeatRays = 64;
 constexpr int kFeatRaysSmall = 16;
 constexpr int64_t kFeatSmallMaxRays = 65536;   // up to 4,096 blocks of 16 rays
 
+// dn_out (nullable): the input directions are raw and normalised here first (render.py:19, the
+// expression of normalize_kernel), written to dn_out for the MLP: one launch fewer per call.
 template <int RAYS>
 __global__ void __launch_bounds__(256)
 ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ dirs, int64_t R,
                     const float* __restrict__ app, int64_t app_rows, float* __restrict__ feat,
-                    float* __restrict__ encd) {
+                    float* __restrict__ encd, float* __restrict__ dn_out) {
   __shared__ float enc[RAYS][kDirEnc + 1];
   __shared__ float apps[RAYS][kAppDim];
+  __shared__ float dsh[RAYS][3];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * RAYS;
+  if (tid < RAYS) {
+    const int64_t r = imin64(r0 + tid, R - 1);
+    float x = dirs[3 * r], y = dirs[3 * r + 1], z = dirs[3 * r + 2];
+    if (dn_out) {
+      const float n = fmaxf(sqrtf(fmaf(z, z, fmaf(y, y, x * x))), 1e-12f);
+      x = x / n;
+      y = y / n;
+      z = z / n;
+      if (r0 + tid < R) {
+        dn_out[3 * r] = x;
+        dn_out[3 * r + 1] = y;
+        dn_out[3 * r + 2] = z;
+      }
+    }
+    dsh[tid][0] = x;
+    dsh[tid][1] = y;
+    dsh[tid][2] = z;
+  }
+  __syncthreads();
   for (int q = tid; q < RAYS * 3 * kDirLevels; q += 256) {
     const int ray = q / (3 * kDirLevels), ic = q % (3 * kDirLevels);
     const int i = ic / 3, c = ic % 3;
-    const int64_t r = imin64(r0 + ray, R - 1);
     float sn, cs;
-    sincosf(dirs[3 * r + c] * (float)(1 << i), &sn, &cs);
+    sincosf(dsh[ray][c] * (float)(1 << i), &sn, &cs);
     enc[ray][3 + 6 * i + c] = sn;
     enc[ray][6 + 6 * i + c] = cs;
   }
   if (tid < RAYS * 3) {
     const int ray = tid / 3, c = tid % 3;
-    enc[ray][c] = dirs[3 * imin64(r0 + ray, R - 1) + c];
+    enc[ray][c] = dsh[ray][c];
   }
   if (app_rows > 0) {
     for (int q = tid; q < RAYS * kAppDim; q += 256) {
@@ -452,14 +473,14 @@ ray_features_kernel(const float* __restrict__ packed, const float* __restrict__ 
 }
 
 int launch_ray_features(const float* packed, const float* dirs, int64_t R, const float* app,
-                        int64_t app_rows, float* feat, hipStream_t s, float* encd) {
+                        int64_t app_rows, float* feat, hipStream_t s, float* encd, float* dn_out) {
   if (R == 0) return NERF_OK;
   if (R <= kFeatSmallMaxRays)
     hipLaunchKernelGGL(ray_features_kernel<kFeatRaysSmall>, dim3((unsigned)((R + kFeatRaysSmall - 1) / kFeatRaysSmall)),
-                       dim3(256), 0, s, packed, dirs, R, app, app_rows, feat, encd);
+                       dim3(256), 0, s, packed, dirs, R, app, app_rows, feat, encd, dn_out);
   else
     hipLaunchKernelGGL(ray_features_kernel<kFeatRays>, dim3((unsigned)((R + kFeatRays - 1) / kFeatRays)), dim3(256), 0,
-                       s, packed, dirs, R, app, app_rows, feat, encd);
+                       s, packed, dirs, R, app, app_rows, feat, encd, dn_out);
   return check_launch("ray_features_kernel");
 }
 

@@ -3569,11 +3569,11 @@ int nerf_train_forward(const float* packed, const float* rays_o, const float* ra
   auto R = [&](int i) { return (float*)(ws + off[i]); };
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  if ((rc = launch_normalize(rays_d, B, R(T_DIRS), s))) return rc;                                    // render.py:19
+  // the directions normalised (render.py:19) by the ray-feature kernel, which writes them to T_DIRS
+  if ((rc = launch_ray_features(packed, rays_d, B, app, app_rows, R(T_FEAT), s, R(T_ENCD), R(T_DIRS)))) return rc;
   if ((rc = launch_stratified(rays_o, R(T_DIRS), B, (float)near, (float)(far - near), N, t_vals, perturb, t_rand,
                               seed, R(T_Z), nullptr, s)))
     return rc;                                                                                          // :22
-  if ((rc = launch_ray_features(packed, R(T_DIRS), B, app, app_rows, R(T_FEAT), s, R(T_ENCD)))) return rc;
   if ((rc = launch_mlp(packed, rays_o, R(T_DIRS), R(T_Z), B, N, R(T_FEAT), R(T_RGB), R(T_SIG), nullptr, 0, s,
                        R(T_SAVE), R(T_ENCD), (uint32_t*)R(T_MASK))))
     return rc;                                                                                          // :49
