@@ -206,15 +206,20 @@ def measure(args, world, rank, group, ranks):
     if group is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    # the timed steps carry no instrumentation (a stream event between kernels costs the GPU a few us);
+    # the stage split comes from as many instrumented steps after them
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(batches[args.warmup + i], True)
+        step(batches[args.warmup + i], False)
     torch.cuda.synchronize()
     if group is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     rank_ms = gather_rank_ms(1e3 * elapsed / args.steps, group)
     elapsed = max(rank_ms) * args.steps * 1e-3
+    for i in range(args.steps):
+        step(batches[args.warmup + i], True)
+    torch.cuda.synchronize()
     stage = {"fwd": [], "bwd": [], "allreduce": [], "adam": []}
     for m in pending:
         stage["fwd"].append(m[0].elapsed_time(m[1]))
