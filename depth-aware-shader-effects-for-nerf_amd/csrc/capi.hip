@@ -140,9 +140,11 @@ static_assert(kS16Consts <= 256, "one block zeroes the constant slots");
 // combine in LDS and one thread per block merges them into the layer's slots by atomicMax on the
 // float bits (non-negative floats order as unsigned integers: exact in any order).  8 blocks per
 // layer: 8 atomics per slot (one atomic per wave and row serialised at L2: 47 us -> a few).  The raw
-// maxima land in the constants' own slots (zeroed first) and scale16_finalize_kernel turns them
-// into the constants.
+// maxima land in the constants' own slots (zeroed by pack_kernel) and the last block to finish turns
+// them into the constants.
 constexpr int kS16RowsPerWave = 8;
+constexpr int kS16Counter = kS16Consts - 1;   // (an unused constant slot: scale16_kernel's block counter)
+static_assert(kS16Counter >= kS16B + 8, "the counter slot is unused by the constants");
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
   __shared__ float red[3][4];
   const int L = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -191,16 +193,26 @@ __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __rest
       atomicMax(cw + kS16R + L, __float_as_uint(l1m));
       atomicMax(cw + kS16B + L, __float_as_uint(bm));
     }
+    // the last block to finish turns the maxima into the constants (scale16_finalize_kernel's work,
+    // without its launch); the block counter sits in the last constant slot (zeroed by pack_kernel,
+    // reset to 0 here, so the packed buffer ends as the host pack writes it)
+    __threadfence();
+    red[0][0] = __uint_as_float(atomicAdd(cw + kS16Counter, 1u) == gridDim.x * gridDim.y - 1 ? 1u : 0u);
   }
-}
-
-__global__ void scale16_finalize_kernel(float* __restrict__ packed) {
-  const int L = threadIdx.x;
-  if (L >= kS16Layers) return;
-  float* consts = packed + kOffScale16;
-  const float mx = consts[kS16Sw + L];
-  const float l1 = L < 8 ? consts[kS16R + L] : 0.0f, bm = L < 8 ? consts[kS16B + L] : 0.0f;
-  store_layer_consts(consts, L, mx, l1, bm);
+  __syncthreads();
+  if (red[0][0] == 0.0f) return;   // (uniform: the flag is the block's own)
+  __threadfence();
+  unsigned* cw = reinterpret_cast<unsigned*>(packed + kOffScale16);
+  const int Lf = threadIdx.x;
+  if (Lf < kS16Layers) {
+    const float mxf = __uint_as_float(__hip_atomic_load(cw + kS16Sw + Lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const float l1f = Lf < 8 ? __uint_as_float(__hip_atomic_load(cw + kS16R + Lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                             : 0.0f;
+    const float bmf = Lf < 8 ? __uint_as_float(__hip_atomic_load(cw + kS16B + Lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                             : 0.0f;
+    store_layer_consts(packed + kOffScale16, Lf, mxf, l1f, bmf);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cw + kS16Counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(256) pack16_kernel(ParamPtrs P, float* __restrict__ packed) {
@@ -216,8 +228,6 @@ int launch_pack(const float* const* params, float* packed, hipStream_t s) {
   if (int rc = check_launch("pack_kernel")) return rc;
   hipLaunchKernelGGL(scale16_kernel, dim3(kHidden / (4 * kS16RowsPerWave), kS16Layers), dim3(256), 0, s, P, packed);
   if (int rc = check_launch("scale16_kernel")) return rc;
-  hipLaunchKernelGGL(scale16_finalize_kernel, dim3(1), dim3(64), 0, s, packed);
-  if (int rc = check_launch("scale16_finalize_kernel")) return rc;
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((kFragFloats + 255) / 256)), dim3(256), 0, s, P, packed);
   return check_launch("pack16_kernel");
 }
