@@ -2448,6 +2448,8 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
 // stages ahead; the x split runs just before its stage's MFMAs (one fragment set, not two).
 // nrows < 256 (the dir/density launch: 160): a columns from nrows on are not read (zeros) and
 // output rows from nrows on are not stored; the partial has nrows rows (wgrad_stride(nrows, 256)).
+// The bias column: each a column has two threads (samples 0-7 and 8-15 of every stage), each summing
+// in double; their sums are added once at the end (wgrad_h16w_kernel: one thread, all 16).
 template <int NS>
 __global__ void __launch_bounds__(256, 2)
 wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
