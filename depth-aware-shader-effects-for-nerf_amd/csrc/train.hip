@@ -271,38 +271,25 @@ NERF_HD inline uint32_t packT16_word(const float* const* P, const float* consts,
 
 struct ParamPtrsT { const float* p[P_COUNT]; };
 
+// (the last block also zeroes the split stream's constant slots, which statsT16_kernel's atomics fill)
 __global__ void __launch_bounds__(256) packT_kernel(ParamPtrsT P, float* __restrict__ packed) {
+  if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < kT16Consts) packed[kOffT16Consts + threadIdx.x] = 0.0f;
+    return;
+  }
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < kPackedT32Floats) packed[e] = packT_value(P.p, e);
 }
 
-// max |W^T| of matrix mt (= max |W| over its columns i < kHidden), 8 rows of W^T per block
-// (thread = row i, coalesced over i), combined by atomicMax on the float bits (exact in any order)
-// into consts[mt] (zeroed first); scaleT16_finalize_kernel turns the maxima into s_w and 1/s_w.
-__global__ void __launch_bounds__(256) scaleT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
-  const int mt = blockIdx.y, i = threadIdx.x;
-  const int outs = mt == 7 ? kDirHidden : kHidden;
-  const int o0 = blockIdx.x * 8;
-  float m = 0.0f;
-  for (int o = o0; o < o0 + 8 && o < outs; ++o) m = fmaxf(m, fabsf(tmat_weight(P.p, mt, i, o)));
-  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-  if ((threadIdx.x & 63) == 0)
-    atomicMax(reinterpret_cast<unsigned*>(packed + kOffT16Consts) + mt, __float_as_uint(m));
-}
-
-__global__ void scaleT16_finalize_kernel(float* __restrict__ packed) {
-  const int mt = threadIdx.x;
-  if (mt < 8) {
-    store_t16_consts(packed + kOffT16Consts, mt, packed[kOffT16Consts + mt]);
-    packed[kOffT16Consts + kT16C + mt] *= 1.0001f;     // rounding margin on the float sums: a bound
-  }
-}
-
+// Statistics of the split scales (statsT16_kernel below): max |W^T| of matrix mt (= max |W| over its
+// columns i < kHidden), 8 rows of W^T per block (thread = row i, coalesced over i), combined by
+// atomicMax on the float bits (exact in any order) into consts[mt] (zeroed first); the last block
+// turns the maxima into s_w and 1/s_w.
 // Row L1 norm of W^T (a forward input neuron's weights over the outputs): four partial sums over
 // the output quarters, each in order, added in order (the host's tmat_row_l1 is the same
 // expression, so device and host constants are bit-identical); the matrix's maximum by atomicMax on
 // the float bits (exact in any order).  One block per (matrix, 64 rows): thread = (row, quarter).
-// Block 32 takes max |density_head.weight|.
+// One more block takes max |density_head.weight|.
 NERF_HD inline float tmat_row_l1_part(const float* const* P, int mt, int i, int q) {
   const int outs = mt == 7 ? kDirHidden : kHidden, per = outs / 4;
   float l1 = 0.0f;
@@ -313,23 +300,63 @@ NERF_HD inline float tmat_row_l1(const float* const* P, int mt, int i) {
   return ((tmat_row_l1_part(P, mt, i, 0) + tmat_row_l1_part(P, mt, i, 1)) + tmat_row_l1_part(P, mt, i, 2)) +
          tmat_row_l1_part(P, mt, i, 3);
 }
-__global__ void __launch_bounds__(256) boundT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
+
+// The three statistics passes in one launch (formerly scaleT16 / boundT16 / finalize kernels): the
+// block counter (an unused constant slot, zeroed by packT_kernel, reset after) elects the last block
+// to finish, which turns the maxima into the constants.  Blocks 0..255: max |W^T| (matrix b / 32,
+// outputs 8 (b % 32) ..); 256..287: row L1 norms (matrix (b - 256) / 4); 288: max |density weight|.
+constexpr int kT16Counter = kT16Consts - 1;
+static_assert(kT16Counter > kT16WsigMax, "the counter slot is unused by the constants");
+__global__ void __launch_bounds__(256) statsT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
   __shared__ float part[4][64];
+  __shared__ unsigned last;
   unsigned* c = reinterpret_cast<unsigned*>(packed + kOffT16Consts);
-  if (blockIdx.x == 32) {
+  const int b = blockIdx.x;
+  if (b < 256) {
+    const int mt = b / 32, i = threadIdx.x;
+    const int outs = mt == 7 ? kDirHidden : kHidden;
+    const int o0 = (b % 32) * 8;
+    float m = 0.0f;
+    for (int o = o0; o < o0 + 8 && o < outs; ++o) m = fmaxf(m, fabsf(tmat_weight(P.p, mt, i, o)));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) {
+      atomicMax(c + mt, __float_as_uint(m));
+      __threadfence();
+    }
+  } else if (b == 256 + 32) {
     float v = fabsf(P.p[P_SIGMA_W][threadIdx.x]);
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-    if ((threadIdx.x & 63) == 0) atomicMax(c + kT16WsigMax, __float_as_uint(v));
-    return;
+    if ((threadIdx.x & 63) == 0) {
+      atomicMax(c + kT16WsigMax, __float_as_uint(v));
+      __threadfence();
+    }
+  } else {
+    const int bb = b - 256, mt = bb >> 2, r = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int i = (bb & 3) * 64 + r;
+    part[q][r] = tmat_row_l1_part(P.p, mt, i, q);
+    __syncthreads();
+    if (q == 0) {
+      float v = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
+      for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+      if (r == 0) {
+        atomicMax(c + kT16C + mt, __float_as_uint(v));
+        __threadfence();
+      }
+    }
   }
-  const int mt = blockIdx.x >> 2, r = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int i = (blockIdx.x & 3) * 64 + r;
-  part[q][r] = tmat_row_l1_part(P.p, mt, i, q);
   __syncthreads();
-  if (q != 0) return;
-  float v = ((part[0][r] + part[1][r]) + part[2][r]) + part[3][r];
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-  if (r == 0) atomicMax(c + kT16C + mt, __float_as_uint(v));
+  if (threadIdx.x == 0) last = atomicAdd(c + kT16Counter, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;   // (uniform)
+  __threadfence();
+  if (threadIdx.x < 8) {
+    const int mt = threadIdx.x;
+    const float mx = __uint_as_float(__hip_atomic_load(c + mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const float l1 = __uint_as_float(__hip_atomic_load(c + kT16C + mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    store_t16_consts(packed + kOffT16Consts, mt, mx);
+    packed[kOffT16Consts + kT16C + mt] = l1 * 1.0001f;   // rounding margin on the float sums: a bound
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(c + kT16Counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __restrict__ packed) {
@@ -341,16 +368,10 @@ __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __res
 int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
   ParamPtrsT P;
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
-  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256)), dim3(256), 0, s, P, packedT);
+  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256 + 1)), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("packT_kernel")) return rc;
-  if (hipMemsetAsync(packedT + kOffT16Consts, 0, kT16Consts * sizeof(float), s) != hipSuccess)
-    return set_error(NERF_ERR_HIP, "packT: hipMemsetAsync failed");
-  hipLaunchKernelGGL(scaleT16_kernel, dim3(kHidden / 8, 8), dim3(256), 0, s, P, packedT);
-  if (int rc = check_launch("scaleT16_kernel")) return rc;
-  hipLaunchKernelGGL(boundT16_kernel, dim3(33), dim3(256), 0, s, P, packedT);
-  if (int rc = check_launch("boundT16_kernel")) return rc;
-  hipLaunchKernelGGL(scaleT16_finalize_kernel, dim3(1), dim3(64), 0, s, packedT);
-  if (int rc = check_launch("scaleT16_finalize_kernel")) return rc;
+  hipLaunchKernelGGL(statsT16_kernel, dim3(256 + 33), dim3(256), 0, s, P, packedT);
+  if (int rc = check_launch("statsT16_kernel")) return rc;
   const size_t words = kOffT16Consts - kPackedT32Floats;
   hipLaunchKernelGGL(packT16_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, packedT);
   return check_launch("packT16_kernel");
