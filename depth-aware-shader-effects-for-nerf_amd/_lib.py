@@ -91,8 +91,6 @@ _SIGNATURES = {
     "nerf_packed_transposed_floats": (ctypes.c_size_t, []),
     "nerf_pack_weights_transposed": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
                                                     ctypes.c_void_p]),
-    "nerf_pack_weights_transposed_split": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
-                                                          ctypes.c_void_p]),
     "nerf_pack_weights_transposed_host": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "nerf_ray_features_train": (ctypes.c_int, [_V, _V, _I64, _V, _I64, _V, _V, _V]),
     "nerf_mlp_forward_train": (ctypes.c_int, [_V, _V, _V, _V, _I64, ctypes.c_int, _V, _V, _V, _V, _V, _V, _V]),
@@ -126,7 +124,7 @@ _SIGNATURES = {
 }
 
 EXPORTED = tuple(_SIGNATURES)
-ABI_VERSION = 12
+ABI_VERSION = 11
 
 _lib = None
 

@@ -365,13 +365,10 @@ __global__ void __launch_bounds__(256) packT16_kernel(ParamPtrsT P, float* __res
     reinterpret_cast<uint32_t*>(packed)[kPackedT32Floats + w] = packT16_word(P.p, packed + kOffT16Consts, w);
 }
 
-// split16: only the split-f16 part and its constants (what the f16x3 data-gradient kernel reads): the
-// pack kernel then runs just its last block, which zeroes the constant slots.
-int launch_packT(const float* const* params, float* packedT, hipStream_t s, bool split16 = false) {
+int launch_packT(const float* const* params, float* packedT, hipStream_t s) {
   ParamPtrsT P;
   for (int i = 0; i < P_COUNT; ++i) P.p[i] = params[i];
-  hipLaunchKernelGGL(packT_kernel, dim3(split16 ? 1u : (unsigned)((kPackedT32Floats + 255) / 256 + 1)), dim3(256), 0, s, P,
-                     packedT);
+  hipLaunchKernelGGL(packT_kernel, dim3((unsigned)((kPackedT32Floats + 255) / 256 + 1)), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("packT_kernel")) return rc;
   hipLaunchKernelGGL(statsT16_kernel, dim3(256 + 33), dim3(256), 0, s, P, packedT);
   if (int rc = check_launch("statsT16_kernel")) return rc;
@@ -3295,12 +3292,6 @@ int nerf_pack_weights_transposed(const float* const* params, float* packedT, ner
   TREQUIRE(params && packedT, "nerf_pack_weights_transposed: null pointer");
   for (int i = 0; i < P_COUNT; ++i) TREQUIRE(params[i], "nerf_pack_weights_transposed: parameter %d is null", i);
   return launch_packT(params, packedT, (hipStream_t)stream);
-}
-
-int nerf_pack_weights_transposed_split(const float* const* params, float* packedT, nerf_stream_t stream) {
-  TREQUIRE(params && packedT, "nerf_pack_weights_transposed_split: null pointer");
-  for (int i = 0; i < P_COUNT; ++i) TREQUIRE(params[i], "nerf_pack_weights_transposed_split: parameter %d is null", i);
-  return launch_packT(params, packedT, (hipStream_t)stream, true);
 }
 
 int nerf_pack_weights_transposed_host(const float* const* params, float* packedT) {

@@ -115,7 +115,6 @@ class Trainer:
         self._tvals = {}
         self._side = None          # side stream for the transposed packing (forward_backward)
         self._side_on = os.environ.get("NERFMI_PACKT_SIDE", "1") != "0"   # (0: same-box A/B)
-        self._packT_full = os.environ.get("NERFMI_PACKT_FULL", "0") == "1"
 
     def view(self, buf, i):
         return buf[self.offsets[i]: self.offsets[i + 1]].view(self.shapes[i])
@@ -152,11 +151,8 @@ class Trainer:
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self._fork.record(main)
         self._side.wait_event(self._fork)
-        # under f16x3 the data gradients read only the split-f16 part (a third of the packing work beside
-        # the forward); NERFMI_PACKT_FULL=1 packs all of it (A/B)
-        packT = lib.nerf_pack_weights_transposed_split if (_lib.get_mlp_arith() == "f16x3" and not self._packT_full) \
-            else lib.nerf_pack_weights_transposed
-        _lib.check(packT(self.param_ptrs, P(self.packedT), self._side.cuda_stream), "nerf_pack_weights_transposed")
+        _lib.check(lib.nerf_pack_weights_transposed(self.param_ptrs, P(self.packedT), self._side.cuda_stream),
+                   "nerf_pack_weights_transposed")
         if self.app_grad is not None:    # the table's gradient is one row this step: zeroed beside the forward
             with torch.cuda.stream(self._side):
                 self.app_grad.zero_()

@@ -48,8 +48,7 @@ const char* nerf_last_error(void);
  * nerf_composite_backward_grad; 10: tile-major save / gradient rows, NERF_TILE_ROWS, and the
  * two-stream nerf_param_grads with its larger workspace; 11: nerf_render_chunk_rays (calls past
  * the launch-size limit run in ray chunks), block exponent records in the save / gradient rows'
- * padding, the split-f16 weight gradient; 12: nerf_pack_weights_transposed_split and the param-grads
- * workspace's chunk partials of the two-workgroups-per-CU weight gradient). */
+ * padding, the split-f16 weight gradient). */
 int nerf_abi_version(void);
 
 /* ------------------------------------------------------------------ R1 rays

@@ -66,10 +66,6 @@ int nerf_train_backward(const float* packed, const float* packedT, const float* 
 /* W^T of trunk layers 1..7 and of dir_linear's h-part in MFMA fragment layout. */
 size_t nerf_packed_transposed_floats(void);
 int nerf_pack_weights_transposed(const float* const* params, float* packedT, nerf_stream_t stream);
-/* ABI 12: only the split-f16 part of packedT and its constants (what the f16x3 data gradients read;
- * the exact-f32 part is left as it was): a third of nerf_pack_weights_transposed's work, for a
- * training loop under f16x3. */
-int nerf_pack_weights_transposed_split(const float* const* params, float* packedT, nerf_stream_t stream);
 int nerf_pack_weights_transposed_host(const float* const* params, float* packedT);
 
 /* nerf_ray_features plus enc_d (R,32): PE_4(d) (models.py:122), zero-padded. */

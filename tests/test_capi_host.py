@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.EXPORTED), "ctypes signature table out of sync with include/*.h"
-    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.nerf_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_bad_arguments_are_reported_not_launched():

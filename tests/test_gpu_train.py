@@ -154,26 +154,6 @@ def test_device_pack_equals_host_pack(ref_state, scale):
 
 
 # ----------------------------------------------------------------------------- composite backward
-def test_split_transposed_pack_matches_full(ref_state):
-    """nerf_pack_weights_transposed_split writes the split-f16 part of packedT and its constants exactly
-    as nerf_pack_weights_transposed does, and leaves the exact-f32 part untouched."""
-    L = _lib()
-    lib, dev = L.load(), L.device()
-    ts = [ref_state[k].to(dev).contiguous() for k in O.STATE_KEYS]
-    arr = (ctypes.c_void_p * 24)(*[t.data_ptr() for t in ts])
-    n = lib.nerf_packed_transposed_floats()
-    full = torch.zeros(n, device=dev)
-    L.check(lib.nerf_pack_weights_transposed(arr, L.ptr(full), L.stream()), "packT")
-    sentinel = 0x7FC01234                 # (a word whose high f16 half is a NaN: no packed weight pair)
-    split = torch.full((n,), sentinel, dtype=torch.int32, device=dev)
-    L.check(lib.nerf_pack_weights_transposed_split(arr, L.ptr(split), L.stream()), "packT split")
-    torch.cuda.synchronize()
-    untouched = (split == sentinel).cpu()
-    f32_floats = int(untouched.int().argmin().item())          # the first word the split pack wrote
-    assert f32_floats > 0 and bool(untouched[:f32_floats].all()) and not bool(untouched[f32_floats:].any())
-    assert torch.equal(split[f32_floats:], full[f32_floats:].view(torch.int32))
-
-
 @pytest.mark.parametrize("N", [1, 2, 7, 64, 100, 200])
 def test_composite_backward_matches_autograd(N):
     L = _lib()
