@@ -337,7 +337,8 @@ def main():
     # --- training leg (BASELINE config 5), every rank: data parallel over the same group
     train = None
     if not args.no_train:
-        targs = argparse.Namespace(steps=args.train_steps, warmup=3, batch=4096, arith=args.arith,
+        # (10 untimed steps: after 3 the step still runs ~2 % slow, profiles/r05/train_warmup.log)
+        targs = argparse.Namespace(steps=args.train_steps, warmup=10, batch=4096, arith=args.arith,
                                    no_cpu_baseline=args.no_cpu_baseline, cpu_seconds=8.0)
         train = bench_train.measure(targs, world, rank, group, ranks)
         if train is not None:
