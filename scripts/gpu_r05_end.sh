@@ -1,6 +1,6 @@
 # Round 5, last evidence at HEAD: the GPU suite, the driver's bench command (plain), smoke.
-mkdir -p gpurun_out/r05/end4
-O=gpurun_out/r05/end4
+mkdir -p gpurun_out/r05/end5
+O=gpurun_out/r05/end5
 bash scripts/gpu_check.sh pytest_all || exit $?
 cp gpurun_out/pytest_gpu.log $O/pytest_gpu.log
 grep -q "FAILED" $O/pytest_gpu.log && { echo "suite not green"; exit 1; }
