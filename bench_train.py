@@ -26,10 +26,9 @@ streamed once, the binding roofline is HBM when its algorithmic bytes (18,188 pe
 (f16x3 default: split-f16 MFMA, peak 2516.8/3 = 838.9 TFLOP/s of fp32-equivalent work; f32:
 157.3).  Under f16x3 the data gradients run on split-f16 MFMA too (838.9) and the weight
 gradients on block-scaled split-f16 MFMA (three f16 products per fp32 product at per-chunk
-power-of-two scales, 838.9; NERFMI_WGRAD=bf16x6: six bf16 products, 419.5); under f32 both run on
-fp32 MFMA (157.3).
-cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on a 1024-ray
-batch on this host's cores.
+power-of-two scales, 838.9); under f32 both run on fp32 MFMA (157.3).
+cpu_baseline: the oracle's train_step (PyTorch-CPU autograd + torch.optim.Adam) on the measured
+config's own batch (--batch, 4096 rays x 64 samples; at least 3 steps) on this host's cores.
 """
 import argparse
 import glob
@@ -51,19 +50,14 @@ FLOP_DGRAD = 2 * (7 * 256 * 256 + 256 * 128)                                   #
 FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 128 + 129 * 3)
 # the weight gradients' MFMA arithmetic under f16x3: the 256-column GEMMs (7 of the 8 big ones and
 # dir/sigma) on split-f16 with per-chunk power-of-two scales (three f16 products per fp32 product:
-# 2516.8/3 = 838.9 TFLOP/s; vendor f16 GEMM 1,323.5 / 3); NERFMI_WGRAD=bf16x6 restores the bf16x6
-# GEMMs (six bf16 products: 2516.8/6 = 419.5 TFLOP/s; vendor bf16 1,377.1 / 6).  The layer-0 and
-# skip-PE GEMMs (K = 63) stay bf16x6 either way.
+# 2516.8/3 = 838.9 TFLOP/s; vendor f16 GEMM 1,323.5 / 3).
 # HBM: bytes the weight-gradient phase must read once per sample (fp32 rows, layout.h): gradient rows
 # d pre_0..7 (8 x 256), [d pre_dir | d sigma] (129), d hd (128), d rgb (3); saved rows enc_x (63),
 # h_0..h_7 (8 x 256), hd (128).  Against 8 TB/s this is the phase's binding roofline under f16x3
 # (0.60 ms per 262,144 samples, against 0.33 ms of MFMA work at 838.9 TFLOP/s).
 HBM_PEAK_GBS = 8000.0
 WGRAD_ALG_BYTES = 4 * (8 * 256 + 129 + 128 + 3 + 63 + 8 * 256 + 128)   # 18,188
-if os.environ.get("NERFMI_WGRAD") == "bf16x6":
-    WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "bf16x6", 6, 1377.1 / 6
-else:
-    WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "block-scaled f16x3", 3, 1323.5 / 3
+WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "block-scaled f16x3", 3, 1323.5 / 3
 
 
 def parse():
@@ -79,7 +73,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(target_s):
+def cpu_baseline(target_s, B=4096, min_steps=3):
     from oracle import nerf_oracle as O
     from nerfmi import cameras
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -89,9 +83,8 @@ def cpu_baseline(target_s):
     o, d = O.get_rays(800, 800, cameras.synthetic_focal(800), cameras.frame_c2w("chair"))
     o, d = o.reshape(-1, 3), d.reshape(-1, 3)
     g = torch.Generator().manual_seed(3)
-    B = 1024
     opt, n, t = None, 0, 0.0
-    while t < target_s and n < 50:
+    while (t < target_s or n < min_steps) and n < 50:
         sel = torch.randperm(o.shape[0], generator=g)[:B]
         t_rand = torch.rand(B, 64, generator=g)
         target = torch.rand(B, 3, generator=g)
@@ -289,7 +282,7 @@ def measure(args, world, rank, group, ranks):
                                                             for k, v in kern.items()} if vendor else None},
                "stage_ms": stage_ms, "phase_ms": kt}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.batch)
     nerfmi.set_mlp_arith(prev_arith)
     del tr, ds, batches
     return out

@@ -147,6 +147,7 @@ constexpr int kS16Counter = kS16Consts - 1;   // (an unused constant slot: scale
 static_assert(kS16Counter >= kS16B + 8, "the counter slot is unused by the constants");
 __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __restrict__ packed) {
   __shared__ float red[3][4];
+  __shared__ unsigned last;          // the block finished last (an integer flag: no float compare)
   const int L = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // the wave's 8 rows loaded first (one memory round trip, not one per row), then per row the lane's
   // column-order sum and the xor tree as before (zeros past a row's end add nothing)
@@ -197,10 +198,10 @@ __global__ void __launch_bounds__(256) scale16_kernel(ParamPtrs P, float* __rest
     // without its launch); the block counter sits in the last constant slot (zeroed by pack_kernel,
     // reset to 0 here, so the packed buffer ends as the host pack writes it)
     __threadfence();
-    red[0][0] = __uint_as_float(atomicAdd(cw + kS16Counter, 1u) == gridDim.x * gridDim.y - 1 ? 1u : 0u);
+    last = atomicAdd(cw + kS16Counter, 1u) == gridDim.x * gridDim.y - 1 ? 1u : 0u;
   }
   __syncthreads();
-  if (red[0][0] == 0.0f) return;   // (uniform: the flag is the block's own)
+  if (last == 0u) return;   // (uniform: the flag is the block's own)
   __threadfence();
   unsigned* cw = reinterpret_cast<unsigned*>(packed + kOffScale16);
   const int Lf = threadIdx.x;
@@ -453,6 +454,9 @@ int nerf_mlp_forward(const float* packed, const float* origins, const float* dir
   REQUIRE(R == 0 || (packed && origins && ray_feat && rgb && sigma && (!z_vals || dirs)),
           "nerf_mlp_forward: null pointer");
   const int64_t rc_rays = nerf_render_chunk_rays(N, 0);
+  if (R > 0 && rc_rays < 1)   // one ray's N samples already exceed the per-launch sample limit
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_mlp_forward: N=%d samples per ray exceed the launch limit %lld", N,
+                     (long long)max_launch_samples());
   for (int64_t r0 = 0; r0 < R; r0 += rc_rays) {            // (one chunk unless R N > 2^30)
     const int64_t n = R - r0 < rc_rays ? R - r0 : rc_rays;
     const int64_t orow = out_slot ? (int64_t)out_T : (int64_t)N;   // output rows per ray
@@ -521,6 +525,8 @@ int nerf_render_rays(const float* packed, const float* rays_o, const float* rays
   REQUIRE(app_rows == 0 || app_rows == 1 || app_rows == B, "nerf_render_rays: app_rows=%lld with B=%lld",
           (long long)app_rows, (long long)B);
   const int64_t chunk = nerf_render_chunk_rays(N, Nf);
+  if (chunk < 1)   // (N + Nf <= 4096 <= the launch limit: unreachable, but never loop on a zero step)
+    return set_error(NERF_ERR_UNSUPPORTED, "nerf_render_rays: N=%d Nf=%d exceed the launch limit", N, Nf);
   const int64_t T = Nf > 0 ? (int64_t)N + Nf : (int64_t)N;   // weights_out / z_out columns
   for (int64_t c0 = 0; c0 < B || (B == 0 && c0 == 0); c0 += chunk) {
     const int64_t n = B - c0 < chunk ? B - c0 : chunk;

@@ -74,14 +74,8 @@ __device__ __forceinline__ uint32_t split_lo_pair(uint32_t hi2, float x0, float 
 // forward with saves 0.99 -> 0.82 ms and the data gradient 0.87 -> 0.71 ms per 262K-sample step, the
 // training step 1.13 -> 1.19 M rays/s (same-box A/B, profiles/r04/ab_train_store_policy.log; sc0 nt
 // the same, sc1 slower).  kRowLoadAux: the weight-gradient GEMMs' once-read row loads.
-#ifndef NERF_ROW_STORE_AUX
-#define NERF_ROW_STORE_AUX 2
-#endif
-#ifndef NERF_ROW_LOAD_AUX
-#define NERF_ROW_LOAD_AUX 0
-#endif
-constexpr int kRowStoreAux = NERF_ROW_STORE_AUX;
-constexpr int kRowLoadAux = NERF_ROW_LOAD_AUX;
+constexpr int kRowStoreAux = 2;
+constexpr int kRowLoadAux = 0;
 
 __device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
 

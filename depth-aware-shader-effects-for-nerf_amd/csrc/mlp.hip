@@ -34,7 +34,7 @@ __device__ unsigned long long nerf_stamps[65536][12];
     unsigned long long t_;                                                                  \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
     __builtin_amdgcn_sched_barrier(0);                                                      \
-    const int64_t w_ = (int64_t)blockIdx.x * NERF_MLP_WAVES + (threadIdx.x >> 6);           \
+    const int64_t w_ = (int64_t)blockIdx.x * kMlpWaves + (threadIdx.x >> 6);           \
     if (w_ < 65536 && (threadIdx.x & 63) == 0) nerf_stamps[w_][i] = t_;                     \
   } while (0)
 #else
@@ -60,12 +60,7 @@ __device__ __forceinline__ f32x16 load_rows(const float* __restrict__ v, int nt,
   return out;
 }
 
-#ifndef NERF_MLP_WAVES
-#define NERF_MLP_WAVES 4      // waves per workgroup (each wave is independent: no barriers, own LDS slice)
-#endif
-#ifndef NERF_MLP_DEPTH
-#define NERF_MLP_DEPTH 8      // weight-fragment blocks in flight per wave
-#endif
+constexpr int kMlpWaves = 4;   // waves per workgroup (each wave is independent: no barriers, own LDS slice)
 
 // One dense layer: NT output tiles of 32 neurons in groups of four, KS_ACT activation k-steps
 // read from `in` (ReLU applied on read when RELU_IN) and KS_PE positional-encoding k-steps
@@ -77,7 +72,7 @@ __device__ __forceinline__ f32x16 load_rows(const float* __restrict__ v, int nt,
 // holds this matrix's first DEPTH blocks of that order, and the last DEPTH loads fetch the
 // first blocks of `next` (the last matrix passes any valid fragment array; those loads go
 // unused; next_ksq is its k-quad count), so no layer starts on an L2 round trip.
-constexpr int kDepth = NERF_MLP_DEPTH;
+constexpr int kDepth = 8;   // weight-fragment blocks in flight per wave
 enum Init { kBias, kPerLane, kAccum };
 
 // packed block index (layout.h frag_elem / 256) of the g-th block of the consumption order
@@ -176,13 +171,13 @@ __device__ __forceinline__ void save_tiles(float* __restrict__ row, int off, con
 // SAVE = the training forward: also writes the per-sample activation row (layout.h kSave*) to
 // `save` (M x kSaveRow); encd (R x 32) holds each ray's PE_4(d) from nerf_ray_features.
 template <bool SAVE>
-__global__ void __launch_bounds__(64 * NERF_MLP_WAVES, 1)
+__global__ void __launch_bounds__(64 * kMlpWaves, 1)
 mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, const float* __restrict__ dirs,
            const float* __restrict__ zv, int64_t M, int N, const float* __restrict__ feat,
            float* __restrict__ rgb, float* __restrict__ sigma, const int* __restrict__ out_slot, int out_T,
            float* __restrict__ save, const float* __restrict__ encd) {
   const int lane = threadIdx.x & 63;
-  const int64_t s0 = ((int64_t)blockIdx.x * NERF_MLP_WAVES + (threadIdx.x >> 6)) * 32;
+  const int64_t s0 = ((int64_t)blockIdx.x * kMlpWaves + (threadIdx.x >> 6)) * 32;
   if (s0 >= M) return;
   const int h = lane >> 5;
   const int64_t s = imin64(s0 + (lane & 31), M - 1);
@@ -204,7 +199,7 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
   // cos on half 1 (models.py:36-44; 2^i x is exact, sin/cos fully range-reduced).  Layer 0
   // reads it from registers; the skip layer reads it back from this wave's LDS slice
   // (32 floats x 64 lanes), so it does not occupy 32 registers through layers 1..3.
-  __shared__ float pe_lds[NERF_MLP_WAVES][kPeSteps][64];
+  __shared__ float pe_lds[kMlpWaves][kPeSteps][64];
   float (*pe_mine)[64] = pe_lds[threadIdx.x >> 6];
   float pe[kPeSteps];
 #pragma unroll
@@ -346,16 +341,16 @@ int launch_mlp(const float* packed, const float* o, const float* d, const float*
   if (M == 0) return NERF_OK;
   if (g_mlp_arith == NERF_ARITH_F16X3)
     return launch_mlp16(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s, save, encd, masks);
-  constexpr int per_block = 32 * NERF_MLP_WAVES;
+  constexpr int per_block = 32 * kMlpWaves;
   const int64_t blocks = (M + per_block - 1) / per_block;
   // tile-major save rows: the last block's rows past M are zeros (layout.h)
   if (save && M % 32 && hipMemsetAsync(save + (M / 32) * 32 * kSaveRow, 0, (size_t)32 * kSaveRow * 4, s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "mlp training forward: hipMemsetAsync failed");
   if (save)
-    hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M, N,
+    hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)blocks), dim3(64 * kMlpWaves), 0, s, packed, o, d, z, M, N,
                        feat, rgb, sigma, out_slot, out_T, save, encd);
   else
-    hipLaunchKernelGGL(mlp_kernel<false>, dim3((unsigned)blocks), dim3(64 * NERF_MLP_WAVES), 0, s, packed, o, d, z, M,
+    hipLaunchKernelGGL(mlp_kernel<false>, dim3((unsigned)blocks), dim3(64 * kMlpWaves), 0, s, packed, o, d, z, M,
                        N, feat, rgb, sigma, out_slot, out_T, nullptr, nullptr);
   return check_launch("mlp_kernel");
 }

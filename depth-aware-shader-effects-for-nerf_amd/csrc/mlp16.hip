@@ -150,12 +150,8 @@ __device__ __forceinline__ void convert4(const f32x16 (&acc)[8], float inv, cons
     }
   }
   if constexpr (SV) {
-#ifndef NERF_FWD_NO_SAVES   // (timing-only A/B builds: without the activation stores / the mask bits)
     save_store(sv, 32 * T + 8 * q, rv);     // tail lanes: offset past the buffer, dropped
-#endif
-#ifndef NERF_FWD_NO_MASKS
     mask_or(sv, T, bits);
-#endif
   }
 }
 // Phase PH of quarter QG (slot J of this half-step's quarter vectors).
@@ -281,16 +277,8 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   wait_vmcnt<8>();                                          // this wave's part of chunk 0 (chunks 1-2 in flight)
   __builtin_amdgcn_s_barrier();
   h16x8 a0[4][2], a1[4][2];
-#ifdef NERF16_ABL_NO_SIDE    // (timing-only: finite stand-in operands)
-  Operand in[16] = {};
-#else
   Operand in[16];
-#endif
   read_kstep<0>(lds, a0, lane);
-#ifdef NERF16_ABL_NO_DSREAD  // (timing-only: real fragments of chunk 0, kept for the whole stream)
-  read_kstep_lds<0>(lds, a0, lane);
-  read_kstep_lds<1>(lds, a1, lane);
-#endif
 
   f32x16 acc[8];
   float m = 0.0f, part = 0.0f;

@@ -635,7 +635,7 @@ __device__ __forceinline__ void fold_mask(uint32_t (&mask)[4], int c, f32x4 a) {
 }
 
 // (Without mask rows: nerf_mlp_backward called with masks = NULL.  The training path runs
-// dgrad16_lds below.)
+// mlp_backward16_bound_kernel below.)
 template <int KS>
 __device__ __forceinline__ void dgrad16(const uint32_t* __restrict__ wmat, const h16x8 (&bh)[16],
                                         const h16x8 (&bl)[16], f32x16 (&out)[8], float inv_w, float inv_g,
@@ -785,214 +785,11 @@ mlp_backward16_kernel(const float* __restrict__ packed, const float* __restrict_
   relu_mask_store(X, mask, gr, 0);
 }
 
-// ---- data gradient with an LDS weight stream (f16x3, mask rows: the training path) ------------
-// The 4 waves of a workgroup read the same W^T fragments.  Loading them per wave (dgrad16) costs
-// 256 one-KiB vector loads per wave and layer.  Here each 16 KiB chunk (2 steps x 4 tiles x
-// {hi, lo} pieces of 1 KiB, the order dgrad16 consumes) is DMA'd once per workgroup
-// (global_load_lds_dwordx4, 4 pieces per wave) into a 4-slot LDS ring, and the fragment reads are
-// software-pipelined as in the forward's stream: a step's MFMAs run while the next step's 8
-// fragments are read, and the barrier that publishes chunk g+1 sits between chunk g's two steps:
-//   [read step 2c+1 (slot g) | MFMA step 2c] wait DMA(g+1), barrier, DMA(g+3) into the slot of
-//   chunk g-1 | [read step 2c+2 (slot g+1) | MFMA step 2c+1]
-// where "publish(g+1)" = wait DMA(g+1), barrier, DMA(g+3): two chunks ahead of the chunk it
-// publishes, into slot (g+3) & 3 = the slot of chunk g-1 in the 4-slot ring.  Invariant: every
-// wave's reads of chunk g-1 fed MFMAs issued before the publish(g+1) barrier (they are the reads of
-// step 2c-1, done by the end of chunk g-1's steps), so the DMA issued right after that barrier
-// overwrites a free slot.  A deeper ring only needs the DMA distance and the slot count kept apart
-// by at least this one chunk.  The
-// stream runs through every layer in consumption order: dir_linear's h-part (8 chunks), then trunk
-// layers 6 .. 0 (16 each).  M0 is set per piece and declared clobbered: nothing else in the kernel
-// reads M0 (as in mlp16.hip's stream).
-struct BwStream {
-  const char* t16;     // packedT
-  const float* ring;   // LDS ring, 4 x 4096 floats
-  uint32_t lds_dma;    // LDS byte address of the ring + 1024 * wave
-  uint32_t voff;       // 16 * lane + 1024 * wave
-};
-
-__device__ __forceinline__ void bw_dma(const BwStream& st, int g) {
-  const size_t layer = g < 8 ? t16_offset(7) : t16_offset(6 - ((g - 8) >> 4));
-  const char* src = st.t16 + layer * 4 + (size_t)(g < 8 ? g : ((g - 8) & 15)) * 16384;
-  const uint32_t dst = st.lds_dma + (uint32_t)(g & 3) * 16384u;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    asm volatile(
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, %1"
-        :
-        : "v"(st.voff), "s"(src + i * 4096), "s"(dst + i * 4096u)
-        : "memory", "m0");
-}
-
-template <int N>
-__device__ __forceinline__ void bw_wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Publish chunk g (own pieces landed: younger than them are chunk g+1's when it exists, and
-// whatever else was issued after those: counting fewer only waits longer), then start chunk g+2.
-__device__ __forceinline__ void bw_publish(const BwStream& bs, int g) {
-  if (g + 1 < kBwChunks) bw_wait_vmcnt<4>();
-  else bw_wait_vmcnt<0>();
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  if (g + 2 < kBwChunks) bw_dma(bs, g + 2);
-}
-
-__device__ __forceinline__ void bw_read_step(const BwStream& bs, int g, int half, u32x4 (&w)[8], int lane) {
-  const float* slot = bs.ring + (g & 3) * 4096 + half * 2048;
-#pragma unroll
-  for (int p = 0; p < 8; ++p) w[p] = *reinterpret_cast<const u32x4*>(slot + p * 256 + lane * 4);
-}
-
-// dgrad16 with the fragments from the ring and the mask from the forward's mask row (mk: this
-// lane's 128 bits of the layer's output mask): this layer's chunks are g0 .. g0 + KS - 1.
-template <int KS>
-__device__ __forceinline__ void dgrad16_lds(const BwStream& bs, int g0, const h16x8 (&bh)[16], const h16x8 (&bl)[16],
-                                            f32x16 (&out)[8], float inv_w, float inv_g, const u32x4& mk,
-                                            uint32_t (&mask)[4], int lane) {
-  u32x4 wa[8], wb[8];
-  bw_publish(bs, g0);
-  bw_read_step(bs, g0, 0, wa, lane);
-  auto step = [&](auto sc, const u32x4 (&w)[8]) __attribute__((always_inline)) {
-    constexpr int st = decltype(sc)::value;
-    constexpr int grp = st / KS, ks = st % KS;
-    if constexpr (ks == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) out[4 * grp + i] = f32x16{};
-    }
-    // small products first: lo(W) hi(g), hi(W) lo(g), then hi(W) hi(g); tiles interleaved
-    sfor<4>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      out[4 * grp + i] = mfma16t(w[2 * i + 1], bh[ks], out[4 * grp + i]);
-    });
-    sfor<4>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      out[4 * grp + i] = mfma16t(w[2 * i], bl[ks], out[4 * grp + i]);
-    });
-    sfor<4>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      out[4 * grp + i] = mfma16t(w[2 * i], bh[ks], out[4 * grp + i]);
-    });
-    if constexpr (ks == KS - 1) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) out[4 * grp + i] = (out[4 * grp + i] * inv_w) * inv_g;
-    }
-  };
-  sfor<KS>([&](auto cc) __attribute__((always_inline)) {
-    constexpr int c = decltype(cc)::value;
-    const int g = g0 + c;
-    bw_read_step(bs, g, 1, wb, lane);
-    step(std::integral_constant<int, 2 * c>{}, wa);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (c + 1 < KS) {
-      bw_publish(bs, g + 1);
-      bw_read_step(bs, g + 1, 0, wa, lane);
-    }
-    step(std::integral_constant<int, 2 * c + 1>{}, wb);
-    __builtin_amdgcn_sched_barrier(0);
-  });
-#pragma unroll
-  for (int i = 0; i < 4; ++i) mask[i] = mk[i];
-}
-
-// The training path's data gradient (f16x3 with mask rows) with the LDS stream: 1.39 -> 1.33 ms
-// per 262K-sample launch against per-wave fragment loads.  Every wave runs to the end (the stream has
-// barriers and every wave moves a quarter of each chunk): a wave past M works on sample M-1 and
-// stores nothing (its gradient-row resource is empty).
-__global__ void __launch_bounds__(256, 1)
-mlp_backward16_lds_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
-                          const uint32_t* __restrict__ masks, const float* __restrict__ sigma,
-                          const float* __restrict__ rgb, const float* __restrict__ dsigma,
-                          const float* __restrict__ drgb, int64_t M, float* __restrict__ grad) {
-  __shared__ __attribute__((aligned(16))) float ring[4 * 4096];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const BwStream bs{reinterpret_cast<const char*>(packedT), ring,
-                    (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)ring + 1024u * wave,
-                    16u * lane + 1024u * wave};
-  bw_dma(bs, 0);
-  bw_dma(bs, 1);
-  const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * 32;   // wave-uniform
-  const int h = lane >> 5;
-  const int64_t s = imin64(s0 + (lane & 31), M - 1);
-  const bool valid = s0 + (lane & 31) < M;
-  float* grow = tile_row(grad, s, kGradRow);
-  const GradRows gr = grad_rows(grad, s0, M, lane);
-  const float* invw = packedT + kOffT16Consts + 8;
-
-  // heads, as mlp_backward_kernel
-  float dv[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float y = rgb[3 * s + c];
-    dv[c] = drgb[3 * s + c] * (y * (1.0f - y));
-  }
-  const float dsp = sigma[s] > 0.0f ? dsigma[s] : 0.0f;
-  if (valid && h == 0) {
-    grow[tile_col(kGradSigma)] = dsp;
-    grow[tile_col(kMetaGradF) + kMetaGradF % 8] = 0.0f;   // no block exponent (layout.h)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) grow[tile_col(kGradRgb) + c] = dv[c];
-  }
-  f32x16 X[8];
-  h16x8 bh[16], bl[16];
-  const float* wr = packed + kOffRgbW;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = t * 32 + 8 * q + 4 * h + e;
-        const float d = fmaf(dv[2], wr[2 * kDirHidden + n], fmaf(dv[1], wr[kDirHidden + n], dv[0] * wr[n]));
-        X[t][4 * q + e] = d;
-        v[e] = d;
-      }
-      grad_store4(gr, kGradHd + t * 32 + 8 * q, v);
-    }
-  // the mask words of every layer up front: an ordinary load waited for after DMA pieces were issued
-  // would wait for those too (hipcc does not count the asm), so none is left pending mid-stream
-  const uint32_t* mrow = masks + s * kMaskRow;
-  u32x4 mks[8];
-#pragma unroll
-  for (int l = 0; l < 8; ++l) mks[l] = *reinterpret_cast<const u32x4*>(mrow + (kMaskLayerBytes * l + 16 * h) / 4);
-  uint32_t mask[4];
-  {
-    const uint32_t* md = mrow + (kMaskRDirByte + 8 * h) / 4;
-    mask[0] = md[0];
-    mask[1] = md[1];
-    relu_mask_store<4>(X, mask, gr, kGradDir);
-  }
-  float inv_g = split_rows<4>(X, bh, bl);
-  dgrad16_lds<kDirHidden / 16>(bs, 0, bh, bl, X, invw[7], inv_g, mks[7], mask, lane);
-  const float* wsg = packed + kOffSigmaW;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(wsg + t * 32 + 8 * q + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) X[t][4 * q + e] = fmaf(dsp, w[e], X[t][4 * q + e]);
-    }
-  // unrolled: a runtime layer index would select mks[] by GPR indexing, which uses M0
-  sfor<7>([&](auto ic) __attribute__((always_inline)) {
-    constexpr int l = 7 - decltype(ic)::value;
-    relu_mask_store(X, mask, gr, l * kHidden);
-    inv_g = split_rows<8>(X, bh, bl);
-    dgrad16_lds<kHidden / 16>(bs, 8 + (7 - l) * 16, bh, bl, X, invw[l - 1], inv_g, mks[l - 1], mask, lane);
-  });
-  relu_mask_store(X, mask, gr, 0);
-}
-
-
 // ---- data gradient with split scales from a bound (f16x3, mask rows: the training path) ---------
-// mlp_backward16_lds_kernel takes each layer's split scale from the exact maximum of the layer's
-// whole gradient row, so no output can be converted before the last MFMA of the layer: the
-// epilogue (mask, row store, maximum, split) sits exposed between layers (PMC: MFMA busy 25 %,
-// 47 % of wave cycles in dependency waits).  Here the scale of d pre_{l-1} = mask . (W_l^T d pre_l)
+// A split scale taken from the exact maximum of the layer's whole gradient row (round 2's kernel,
+// in git history) leaves no output convertible before the last MFMA of the layer: the epilogue
+// (mask, row store, maximum, split) sits exposed between layers (PMC: MFMA busy 25 %, 47 % of wave
+// cycles in dependency waits).  Here the scale of d pre_{l-1} = mask . (W_l^T d pre_l)
 // comes from the bound |W_l^T g| <= C_l max|g|, C_l the largest row L1 norm of W_l^T (pack-time,
 // packedT kT16C), with max|g| the exact maximum of this layer's input, tracked while that input was
 // being converted.  So the schedule is mlp16_kernel's (stream16.h): a layer's 8 output tiles run as
@@ -1049,11 +846,9 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
       xs[e] = d * s;
     }
   }
-#ifndef NERF_BW_NO_STORES   // (timing-only A/B build: the cost of the gradient-row stores)
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
                                          (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice),
                                          kRowStoreAux);
-#endif
   if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
     Operand& op = in[OP0 + QG / 2];
     typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
@@ -1309,15 +1104,9 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
   if (M % 32 && hipMemsetAsync(grad + (M / 32) * 32 * kGradRow, 0, (size_t)32 * kGradRow * 4, s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "mlp backward: hipMemsetAsync failed");
   if (g_mlp_arith == NERF_ARITH_F16X3) {
-#ifndef NERF_BW_EXACT   // the bound-scaled kernel (default; NERF_BW_EXACT: the exact-row-maximum one, A/B)
     if (masks)
       hipLaunchKernelGGL(mlp_backward16_bound_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
-#else
-    if (masks)
-      hipLaunchKernelGGL(mlp_backward16_lds_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
-#endif
     else
       hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, save, sigma, rgb, dsigma, drgb, M, grad);
@@ -1345,21 +1134,11 @@ static inline bool wgrad_whole_tile(int N, int K) { return (N == 256 || N == 160
 // launches are bound by HBM, not MFMA, and halving the chunk partials (~0.5 GB per step written and
 // read back) paid +1.7 % on the training step against 1,024-sample chunks (same-box A/B,
 // profiles/r05/ab_head3_pe_clen2k.log; under bf16x6 the 2,048-sample chunks had been 3.5 % slower).
-#ifndef NERF_WG_WHOLE_CLEN   // (A/B builds: the whole-tile chunk length and minimum chunk count)
-#define NERF_WG_WHOLE_CLEN kWChunk
-#endif
-#ifndef NERF_WG_MIN_CHUNKS
-#define NERF_WG_MIN_CHUNKS 128
-#endif
-#ifndef NERF_K64_CLEN   // (A/B builds: the 512 x 63 pair's chunk length and minimum chunk count)
-#define NERF_K64_CLEN (kWChunk / 2)
-#endif
-#ifndef NERF_K64_MIN_CHUNKS
-#define NERF_K64_MIN_CHUNKS 256
-#endif
+constexpr int kWholeClen = kWChunk, kWholeMinChunks = 128;       // whole-tile chunk length, minimum chunk count
+constexpr int kPairClen = kWChunk / 2, kPairMinChunks = 256;      // the layer-0 / skip-PE pair's
 static inline int wgrad_chunk_len_big(int N, int K) {
-  if (wgrad_whole_tile(N, K)) return NERF_WG_WHOLE_CLEN;   // one block per chunk, 256 per step
-  if (K <= 64 && N == 2 * kHidden) return NERF_K64_CLEN;   // (the layer-0 / skip-PE pair)
+  if (wgrad_whole_tile(N, K)) return kWholeClen;   // one block per chunk, 256 per step
+  if (K <= 64 && N == 2 * kHidden) return kPairClen;   // (the layer-0 / skip-PE pair)
   if (K <= 64 && N > 64) return kWChunk / 2;       // (wgrad_bf_k64_kernel: 512-sample chunks ran the GEMM
                                                     // 3 % faster but doubled the reduction)
   const int tiles = ((N + 127) / 128) * ((K + 127) / 128);
@@ -1369,7 +1148,7 @@ static inline int wgrad_chunk_len_big(int N, int K) {
 // there are >= 256 chunks: 4,096 rays in 1,024-row chunks ran 8 blocks, 80-100 us per launch.
 static inline int wgrad_chunk_len(int N, int K, int64_t M) {
   int c = wgrad_chunk_len_big(N, K);
-  const int min_chunks = wgrad_whole_tile(N, K) ? NERF_WG_MIN_CHUNKS : (K <= 64 && N == 2 * kHidden) ? NERF_K64_MIN_CHUNKS : 256;
+  const int min_chunks = wgrad_whole_tile(N, K) ? kWholeMinChunks : (K <= 64 && N == 2 * kHidden) ? kPairMinChunks : 256;
   while (c > 16 && (M + c - 1) / c < min_chunks) c /= 2;
   return c;
 }
@@ -1817,19 +1596,8 @@ wgrad_bf_kernel(const float* __restrict__ a, int64_t lda, int N, const float* __
   }
 }
 
-// The 256 x 256 trunk layers (N = K = 256, one x row per sample): the whole weight gradient of a
-// chunk in one workgroup of 8 waves (2 per SIMD), each wave a 128 (n) x 64 (k) sub-tile (4 x 2
-// MFMA tiles).  Same arithmetic (bf16x6), same partial layout and deterministic chunk reduction as
-// wgrad_bf_kernel.
-//   x (the B operand: column k, samples 8h .. 8h+7 in lane (k & 31) + 32h) is loaded by each wave
-//   straight in fragment order and split in registers: the two waves of a k range each split it,
-//   and it never touches LDS.
-//   a (the A operand, shared by the four waves of an n half) goes through LDS, split once by the
-//   whole workgroup (thread: one column, 8 samples) into [part][column][sample] rows of 48 bytes.
-// LDS traffic per 16-sample stage: 24 KiB written + 96 KiB of fragment reads (staging x as well
-// cost 48 + 144 KiB, and the MFMAs waited on it).  Loads run two stages ahead, issued
-// unconditionally (a stage past the chunk reads zeros through an empty buffer resource) so the
-// compiler's vmcnt waits count only the older stage.
+// The whole-tile (256 x 256) weight gradients: the trunk layers' d pre_l over h_{l-1}, the skip
+// layer's h3 block and dir/density over h7.
 constexpr int kWT = 256;
 __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll
@@ -1843,338 +1611,9 @@ __device__ __forceinline__ void split3_bf16(const float (&v)[8], bf16x8& p0, bf1
     p2[j] = (__bf16)r2;
   }
 }
-// HALF: the n rows split over two workgroups of 4 waves (one per SIMD), 128 rows each, two per CU:
-// the per-stage barrier then lines up only the 4 waves of one half, and the other workgroup's waves
-// on the same SIMDs (the other half, or another chunk) run out of phase, so one's split (VALU) can
-// run in the other's MFMA shadow.  The two halves of a chunk are launched 8 blocks apart (the same
-// XCD): the chunk's x rows come from HBM once per L2.  (512 threads: both halves in one workgroup.)
-// Timing-only ablation builds (scripts/gpu_r03_*.sh; results are wrong): NERF_WG_NO_ALOAD / _NO_XLOAD
-// replace the operand loads by a constant, NERF_WG_NO_SPLIT the bf16 split by a bit cast.
-#ifdef NERF_WG_NO_ALOAD
-#define WG_LOAD_A(v) (0.5f)
-#else
-#define WG_LOAD_A(v) (v)
-#endif
-#ifdef NERF_WG_NO_XLOAD
-#define WG_LOAD_X(v) (0.25f)
-#else
-#define WG_LOAD_X(v) (v)
-#endif
-#ifdef NERF_WG_NO_SPLIT
-__device__ __forceinline__ void split3_cast(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-  const f32x4 lo = {v[0], v[1], v[2], v[3]};
-  p0 = __builtin_bit_cast(bf16x8, lo);
-  const f32x4 hi = {v[4], v[5], v[6], v[7]};
-  p1 = __builtin_bit_cast(bf16x8, hi);
-  p2 = p0;
-}
-#define WG_SPLIT split3_cast
-#else
-#define WG_SPLIT split3_bf16
-#endif
-template <bool BLK, bool HALF = false>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
-__global__ void __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1)
-wgrad_bf256_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                   int clen, float* __restrict__ partial) {
-  constexpr int NR = HALF ? kWT / 2 : kWT;           // a columns (output rows) of this workgroup
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][NR][kBfRow];
-  __shared__ double bsum[2][NR];
-  const int chunk = HALF ? (int)(blockIdx.x / 16) * 8 + (int)(blockIdx.x % 8) : (int)blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  if (m0 >= M) return;                               // (HALF: the grid's last 16-block group) uniform, before any barrier
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wn = HALF ? (int)(blockIdx.x / 8) % 2 : w & 1, wk = HALF ? w : w >> 1;   // n rows 128 wn .., k columns 64 wk ..
-  const int r0 = HALF ? 0 : 128 * wn;                // this wave's first row in As
-  const int n0 = HALF ? 128 * wn : 0;                // the workgroup's first output row
-  const int h = lane >> 5, c = lane & 31;
-  // a loader: thread tid owns column tid % NR, samples 8 (tid / NR) .. +7 of each stage; sample j
-  // of the octet at voffset avo + soffset j * lda4 (wave-uniform)
-  const int col = tid % NR, oct = tid / NR;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(n0 + col) + col % 8 + 64 * oct)   // (n0 % 8 == 0)
-                          : (uint32_t)(8 * oct) * lda4 + 4u * (uint32_t)(n0 + col);
-  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
-  uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int xc = 64 * wk + 32 * t + c;
-    xvo[t] = BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)xc;
-  }
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[2][8], rx[2][2][8];   // two stages in flight: stage k's values in set k % 2
-  double bacc = 0.0;                 // bias column in double: one rounding per chunk
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
-        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
-        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux)));
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux)));
-  };
-  auto store_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
-    bf16x8 p0, p1, p2;
-    WG_SPLIT(ra[SET], p0, p1, p2);
-    *reinterpret_cast<bf16x8*>(&As[buf][0][col][8 * oct]) = p0;
-    *reinterpret_cast<bf16x8*>(&As[buf][1][col][8 * oct]) = p1;
-    *reinterpret_cast<bf16x8*>(&As[buf][2][col][8 * oct]) = p2;
-  };
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  // an even number of stages (one past the chunk reads zeros): no conditional code in the loop, so
-  // the compiler's vmcnt waits see one pattern of loads
-  const int nstages = (int)((m1 - m0 + 2 * kBfStage - 1) / (2 * kBfStage)) * 2;
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  load(S0{}, 0);
-  load(S1{}, 1);
-  store_a(S0{}, 0);
-  __syncthreads();
-  // iteration st: split stage st's x (set st % 2) into fragments, reuse the set for stage st+2's
-  // loads, stage st's MFMAs (a from LDS buffer st % 2), stage st+1's a into the other buffer
-  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    using Other = std::integral_constant<int, 1 - SET>;
-    const int buf = SET;
-    bf16x8 fx[2][3];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) WG_SPLIT(rx[SET][t], fx[t][0], fx[t][1], fx[t][2]);
-    load(set_c, st + 2);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 fa[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(&As[buf][p][r0 + 32 * i + c][8 * h]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma_bf16(fa[0], fx[j][2], t);
-        t = mfma_bf16(fa[1], fx[j][1], t);
-        t = mfma_bf16(fa[2], fx[j][0], t);
-        t = mfma_bf16(fa[0], fx[j][1], t);
-        t = mfma_bf16(fa[1], fx[j][0], t);
-        acc[i][j] = mfma_bf16(fa[0], fx[j][0], t);
-      }
-    }
-    store_a(Other{}, buf ^ 1);   // (after the last stage: zeros into the idle buffer)
-    __syncthreads();
-  };
-  for (int st = 0; st < nstages; st += 2) {
-    iteration(S0{}, st);
-    iteration(S1{}, st + 1);
-  }
-  constexpr int KP = kWT + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(kWT, kWT);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int nn = 128 * wn + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
-        out[(size_t)nn * KP + kk] = acc[i][j][g];
-      }
-    }
-  // bias column: every staged a value passed through store_a() exactly once (the rest are zeros)
-  bsum[oct][col] = bacc;
-  __syncthreads();
-  if (tid < NR) out[(size_t)(n0 + tid) * KP + kWT] = (float)(bsum[0][tid] + bsum[1][tid]);
-}
-
-// The 256 x 256 weight gradient with one wave per SIMD (mlp16's execution model instead of two
-// waves sharing each SIMD): a workgroup of 4 waves per 1,024-sample chunk, one per CU, each wave the
-// full 256 rows x 64 columns (8 x 2 MFMA tiles, 256 accumulator registers).  With the register file
-// to itself a wave keeps four stages of raw operands in flight (loads three stages ahead) and two
-// sets of split x fragments: stage st's MFMAs run while stage st+1's x and a are split (a into the
-// other LDS buffer) -- the VALU in the MFMA shadow of the same wave, not of a second wave that the
-// per-stage barrier lines up with it.  a: thread t loads column t (16 samples) and splits it once per
-// workgroup; x: each wave its own 64 columns in fragment order.  Same bf16x6 arithmetic, partial
-// layout and double bias column as wgrad_bf256_kernel.
-// NRT: output row tiles (8 = 256 rows; 5 = 160 rows, dir_linear + the density head: the a loader still
-// stages 256 columns, the MFMAs and the partial cover the first 32 NRT rows).
-template <bool BLK, int NRT = 8>
-__global__ void __launch_bounds__(256, 1)
-wgrad_bf256w_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                    int clen, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kWT][kBfRow];
-  const int chunk = blockIdx.x;
-  const int64_t m0 = (int64_t)chunk * clen;
-  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
-  const int tid = threadIdx.x, lane = tid & 63, wk = tid >> 6;   // wave wk: columns 64 wk ..
-  const int h = lane >> 5, c = lane & 31;
-  const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  // a loader: thread t owns column t, the stage's 16 samples: sample j at voffset avo + soffset j * as4
-  const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(tid) + tid % 8) : 4u * (uint32_t)tid;
-  const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
-  uint32_t xvo[2];                                   // x fragment t: column 64 wk + 32 t + c, samples 8h ..
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int xc = 64 * wk + 32 * t + c;
-    xvo[t] = BLK ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : (uint32_t)(8 * h) * ldx4 + 4u * (uint32_t)xc;
-  }
-  const uint32_t mrel_end = (uint32_t)(m1 - m0);
-  float ra[4][16], rx[4][2][8];      // four stages of raw operands: stage k in set k % 4
-  double bacc = 0.0;                 // bias column (column tid), in double
-  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
-    const int64_t ms = m0 + rel0;
-    const bool live = rel0 < mrel_end;   // past the chunk: an empty resource, the loads read zeros
-    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(BLK ? a + (ms / 32) * 32 * lda + (ms % 32) * 8 : a + ms * lda), (short)0,
-        BLK ? (live ? (int)(32 * lda4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * lda4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(BLK ? x + (ms / 32) * 32 * ldx + (ms % 32) * 8 : x + ms * ldx), (short)0,
-        BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      ra[SET][j] = WG_LOAD_A(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux)));
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = WG_LOAD_X(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux)));
-  };
-  bf16x8 fx[2][2][3];                // split x fragments of stages st (fx[st & 1]) and st+1
-  auto split_x = [&](auto set_c, auto fb_c) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value, FB = decltype(fb_c)::value;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) WG_SPLIT(rx[SET][t], fx[FB][t][0], fx[FB][t][1], fx[FB][t][2]);
-  };
-  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) bacc += (double)ra[SET][j];
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ra[SET][8 * o + j];
-      bf16x8 p0, p1, p2;
-      WG_SPLIT(v, p0, p1, p2);
-      *reinterpret_cast<bf16x8*>(&As[buf][0][tid][8 * o]) = p0;
-      *reinterpret_cast<bf16x8*>(&As[buf][1][tid][8 * o]) = p1;
-      *reinterpret_cast<bf16x8*>(&As[buf][2][tid][8 * o]) = p2;
-    }
-  };
-  f32x16 acc[NRT][2];
-#pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i][0] = acc[i][1] = f32x16{};
-  const int nstages = (int)((mrel_end + 4 * kBfStage - 1) / (4 * kBfStage)) * 4;   // a multiple of 4; extras read zeros
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using C2 = std::integral_constant<int, 2>;
-  load(C0{}, 0);
-  load(C1{}, 1);
-  load(C2{}, 2);
-  split_x(C0{}, C0{});
-  split_a(C0{}, 0);
-  __syncthreads();
-  // iteration st (set st % 4, buffers st % 2): stage st+3's loads; stage st's MFMAs with stage st+1's
-  // splits in their shadow; barrier
-  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_c)::value, FB = SET & 1;
-    using Nxt = std::integral_constant<int, (SET + 1) & 3>;
-    using Ld = std::integral_constant<int, (SET + 3) & 3>;
-    using FBn = std::integral_constant<int, FB ^ 1>;
-    load(Ld{}, st + 3);
-    __builtin_amdgcn_sched_barrier(0);
-#ifndef NERF_WG_FRAG_JIT
-    // row tile i's MFMAs run while tile i+1's 3 fragments are read (read just before its own MFMAs,
-    // each tile waited out the LDS latency: ~8 exposed waits per stage)
-    bf16x8 fa[2][3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) fa[0][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][c][8 * h]);
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      if (i + 1 < NRT) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fa[(i + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * (i + 1) + c][8 * h]);
-      }
-      const bf16x8 (&f)[3] = fa[i & 1];
-#else   // A/B: each tile's fragments read just before its MFMAs
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-      bf16x8 f[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(&As[FB][p][32 * i + c][8 * h]);
-#endif
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 t = acc[i][j];
-        t = mfma_bf16(f[0], fx[FB][j][2], t);
-        t = mfma_bf16(f[1], fx[FB][j][1], t);
-        t = mfma_bf16(f[2], fx[FB][j][0], t);
-        t = mfma_bf16(f[0], fx[FB][j][1], t);
-        t = mfma_bf16(f[1], fx[FB][j][0], t);
-        acc[i][j] = mfma_bf16(f[0], fx[FB][j][0], t);
-      }
-    }
-    split_x(Nxt{}, FBn{});
-    split_a(Nxt{}, FB ^ 1);
-    // schedule: per row tile 3 fragment reads (the next tile's, or this tile's under
-    // NERF_WG_FRAG_JIT), then its 12 MFMAs each followed by 2 VALU of the next stage's splits; the
-    // split's LDS writes last
-#ifndef NERF_WG_FRAG_JIT
-    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);         // tile 0's reads
-#endif
-#pragma unroll
-    for (int i = 0; i < NRT; ++i) {
-#ifndef NERF_WG_FRAG_JIT
-      if (i + 1 < NRT) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS reads (tile i+1)
-#else
-      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);       // DS reads
-#endif
-#pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, NRT >= 8 ? 2 : 4, 0);     // VALU
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x200, 6, 0);         // DS writes
-    __syncthreads();
-  };
-  for (int st = 0; st < nstages; st += 4) {
-    iteration(C0{}, st);
-    iteration(C1{}, st + 1);
-    iteration(C2{}, st + 2);
-    iteration(std::integral_constant<int, 3>{}, st + 3);
-  }
-  constexpr int KP = kWT + 1;
-  float* out = partial + (size_t)chunk * wgrad_stride(32 * NRT, kWT);
-#pragma unroll
-  for (int i = 0; i < NRT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kk = 64 * wk + 32 * j + c;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) out[(size_t)(32 * i + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = acc[i][j][g];
-    }
-  if (tid < 32 * NRT) out[(size_t)tid * KP + kWT] = (float)bacc;   // every staged a value passed through split_a once
-}
-
 // ------------------------------------------------- split-f16 ("f16x3") weight gradient, 256 columns
-// The whole-tile GEMM of wgrad_bf256w_kernel on v_mfma_f32_32x32x16_f16 with three products per
-// fp32 product instead of bf16x6's six: every operand value is split as v s = hi + lo (f16 each, lo =
+// The whole-tile GEMM (a chunk's 256 x 256 weight gradient in one workgroup) on
+// v_mfma_f32_32x32x16_f16 with three products per fp32 product instead of bf16x6's six: every operand value is split as v s = hi + lo (f16 each, lo =
 // f16(v s - hi), the residual exact in f32) and a k-step accumulates lo(a)hi(x) + hi(a)lo(x) +
 // hi(a)hi(x) (small terms first; the dropped lo lo term and the split residual are O(2^-22) of the
 // product), half the MFMAs and two thirds of the split VALU of bf16x6.  f16 lacks f32's exponent
@@ -2203,11 +1642,7 @@ __device__ __forceinline__ void split2_f16(const float (&v)[8], float s, h16x8& 
   for (int p = 0; p < 4; ++p) {
     const float x0 = v[2 * p] * s, x1 = v[2 * p + 1] * s;
     const h16x2 hi2 = {(_Float16)x0, (_Float16)x1};
-#ifdef NERF_WG_ABL_NOSPLIT
-    const h16x2 lo2 = {(_Float16)0.0f, (_Float16)0.0f};
-#else
     const h16x2 lo2 = __builtin_bit_cast(h16x2, split_lo_pair(__builtin_bit_cast(uint32_t, hi2), x0, x1));
-#endif
     hi[2 * p] = hi2[0];
     hi[2 * p + 1] = hi2[1];
     lo[2 * p] = lo2[0];
@@ -2283,24 +1718,6 @@ __device__ __forceinline__ void h16_chunk_exps(const float* __restrict__ a, int6
   Ex = __builtin_amdgcn_readfirstlane(Ex < kH16EMin ? kH16EMin : Ex);
 }
 
-// Ablation builds of the whole-tile split-f16 weight gradient (wrong results; timing only):
-// NERF_WG_ABL_NOLOAD (operands from registers, no global loads), NERF_WG_ABL_MFMA1 (the hi x hi product only),
-// NERF_WG_ABL_NOBIAS (no double bias sums), NERF_WG_ABL_NOSPLIT (hi parts only, lo = 0).
-#ifdef NERF_WG_ABL_NOLOAD
-#define WG_ABL_LOAD(v) ((float)(rel0 + j) * 1e-3f)
-#else
-#define WG_ABL_LOAD(v) (v)
-#endif
-#ifdef NERF_WG_ABL_MFMA1
-#define WG_ABL_MFMA(e) ((void)0)
-#else
-#define WG_ABL_MFMA(e) (e)
-#endif
-#ifdef NERF_WG_ABL_NOBIAS
-#define WG_ABL_BIAS(e) ((void)0)
-#else
-#define WG_ABL_BIAS(e) (e)
-#endif
 typedef _Float16 H16Stage[2][2][kWT][kBfRow];   // [buffer][hi, lo][column][sample]
 template <bool BLK, int NRT>
 __device__ __forceinline__ void h16w_chunk(const float* __restrict__ a, int64_t lda, const float* __restrict__ x,
@@ -2336,12 +1753,12 @@ __device__ __forceinline__ void h16w_chunk(const float* __restrict__ a, int64_t 
         BLK ? (live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0) : (int)((mrel_end - rel0) * ldx4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      ra[SET][j] = WG_ABL_LOAD(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux)));
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, (int)(j * as4), kRowLoadAux));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = WG_ABL_LOAD(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux)));
+        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], (int)(j * xs4), kRowLoadAux));
   };
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
@@ -2361,7 +1778,7 @@ __device__ __forceinline__ void h16w_chunk(const float* __restrict__ a, int64_t 
   auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) WG_ABL_BIAS(bacc += (double)ra[SET][j]);
+    for (int j = 0; j < 16; ++j) bacc += (double)ra[SET][j];
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
       float v[8];
@@ -2406,8 +1823,8 @@ __device__ __forceinline__ void h16w_chunk(const float* __restrict__ a, int64_t 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x16 t = acc[i][j];
-        WG_ABL_MFMA(t = mfma16(f[1], fx[FB][j][0], t));
-        WG_ABL_MFMA(t = mfma16(f[0], fx[FB][j][1], t));
+        t = mfma16(f[1], fx[FB][j][0], t);
+        t = mfma16(f[0], fx[FB][j][1], t);
         acc[i][j] = mfma16(f[0], fx[FB][j][0], t);
       }
     }
@@ -2848,12 +2265,9 @@ struct WgradSplit {                  // rows n0 <= n < n_end of a weight gradien
 // split.out_b[n - n0] instead.  A workgroup owns 64 float4 columns of the partial layout; its
 // kRedParts waves each sum a contiguous 1/kRedParts of the chunks (fixed order, eight loads in flight
 // per lane), then the parts are added in order: deterministic.  The reductions run beside the other
-// stream's GEMMs: eight waves per workgroup (NERF_RED_PARTS=8) made the step 2-3 % slower than four
-// (same-box A/B, profiles/r03_ab_train_reduce_parts.log).
-#ifndef NERF_RED_PARTS
-#define NERF_RED_PARTS 4
-#endif
-constexpr int kRedParts = NERF_RED_PARTS;
+// stream's GEMMs: eight waves per workgroup made the step 2-3 % slower than four (same-box A/B,
+// profiles/r03_ab_train_reduce_parts.log).
+constexpr int kRedParts = 4;
 __device__ __forceinline__ void wgrad_reduce_body(const float* __restrict__ partial, int chunks, int N, int K,
                                                   float* __restrict__ out_w, int ldo, float* __restrict__ out_b,
                                                   int accumulate, const WgradSplit& split, int scaled) {
@@ -2995,29 +2409,6 @@ static int launch_wgrad_pe_pair(const float* save, const float* grad, int64_t M,
   return check_launch("wgrad_reduce_kernel");
 }
 
-// The 256-column weight gradients of the split arithmetic run on split-f16 MFMA (wgrad_h16w_kernel)
-// unless NERFMI_WGRAD=bf16x6 is set (read once; the bf16x6 kernel is kept for same-process A/Bs).
-static bool wgrad_h16() {
-  static const bool on = [] {
-    const char* e = getenv("NERFMI_WGRAD");
-    return !(e && strcmp(e, "bf16x6") == 0);
-  }();
-  return on;
-}
-// The hidden layers' and the dir/density launch's split-f16 GEMMs run on wgrad_h16h_kernel<3> (two
-// workgroups per CU, half the rows each); NERFMI_WGRAD_HALF=0 selects wgrad_h16w_kernel (one workgroup
-// per CU) for both and =2 the two-set ring, for same-process A/Bs (profiles/r05/ab_wgrad_half.log,
-// ab_wgrad_dir.log).
-static int wgrad_half() {
-  static const int ns = [] {
-    const char* e = getenv("NERFMI_WGRAD_HALF");
-    if (e && strcmp(e, "0") == 0) return 0;
-    if (e && strcmp(e, "2") == 0) return 2;
-    return 3;
-  }();
-  return ns;
-}
-
 // tiled: a (and x when x_div == 1 and x_tiled) are tile-major rows (layout.h) of row length lda / ldx,
 // each pointer at its slice's tile_col; the training path (param_grads).  Otherwise row-major.  The
 // appearance projection's x (the embedding rows, one per ray) is row-major: x_tiled = false.
@@ -3036,55 +2427,22 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
   const bool x_blk = tiled && x_tiled && x_div == 1;   // x tile-major
   int rc;
   bool scaled = false;                                  // partials of wgrad_h16w_kernel (chunk exponents)
-  // the split arithmetic: bf16x6 MFMA (buffer offsets of a chunk's rows must stay below 2^31)
+  // the split arithmetic (buffer offsets of a chunk's rows must stay below 2^31): the whole-tile
+  // GEMMs on split-f16 MFMA, the rest on bf16x6
   if (g_mlp_arith == NERF_ARITH_F16X3 && K >= 1 && lda < (1 << 18) && ldx < (1 << 18)) {
     const int clen = wgrad_chunk_len(N, K, M);
     chunks = (int)((M + clen - 1) / clen);
-    const bool h16 = wgrad_h16();
-    if (N == 160 && wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {   // dir_linear + density head
-      if (h16 && wgrad_half() == 3)   // two workgroups per CU, 160 of 256 rows kept
-        hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, N, hm, ws);
-      else if (h16)
-        hipLaunchKernelGGL((wgrad_h16w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
-                           hm, ws);
-      else
-        hipLaunchKernelGGL((wgrad_bf256w_kernel<true, 5>), dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen,
-                           ws);
-      rc = check_launch("wgrad whole-tile <5>");
-      scaled = h16;
-    } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk) && h16) {
-      if (tiled && wgrad_half() == 2)
-        hipLaunchKernelGGL(wgrad_h16h_kernel<2>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, kWT, hm, ws);
-      else if (tiled && wgrad_half() == 3)
-        hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                           clen, chunks, kWT, hm, ws);
-      else if (tiled)
-        hipLaunchKernelGGL(wgrad_h16w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
-      else
-        hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
+    if (wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {
+      // tile-major rows (the training path): two workgroups per CU, half the rows each; the
+      // dir_linear + density launch (N = 160) keeps 160 of 256 rows
+      hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
+                         clen, chunks, N, hm, ws);
+      rc = check_launch("wgrad_h16h_kernel");
+      scaled = true;
+    } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && !tiled) {   // nerf_wgrad's row-major operands
+      hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       rc = check_launch("wgrad_h16w_kernel");
       scaled = true;
-    } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && (!tiled || x_blk)) {
-#if !defined(NERF_WG_HALF) && !defined(NERF_WG_WHOLE)   // one wave per SIMD, 4-stage prefetch (default)
-      if (tiled)
-        hipLaunchKernelGGL(wgrad_bf256w_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-      else
-        hipLaunchKernelGGL(wgrad_bf256w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-#elif defined(NERF_WG_HALF)   // A/B: two 4-wave workgroups per chunk (NERF_WG_WHOLE: one of 8 waves)
-      const unsigned hb = (unsigned)((chunks + 7) / 8) * 16;
-      if (tiled)
-        hipLaunchKernelGGL((wgrad_bf256_kernel<true, true>), dim3(hb), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-      else
-        hipLaunchKernelGGL((wgrad_bf256_kernel<false, true>), dim3(hb), dim3(256), 0, s, a, lda, x, ldx, M, clen, ws);
-#else
-      if (tiled)
-        hipLaunchKernelGGL(wgrad_bf256_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
-      else
-        hipLaunchKernelGGL(wgrad_bf256_kernel<false>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, M, clen, ws);
-#endif
-      rc = check_launch("wgrad_bf256_kernel");
     } else if (N == kWT && K <= 64 && x_div == 1 && (!tiled || x_blk)) {
       if (tiled)
         hipLaunchKernelGGL(wgrad_bf_k64_kernel<true>, dim3((unsigned)chunks), dim3(512), 0, s, a, lda, x, ldx, K, M,
@@ -3437,22 +2795,19 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   };
   static_assert(kSaveEncX == save_h(3) + kHidden, "the skip layer's input [h3 | enc_x] is contiguous in the save row");
   int rc;
-#ifndef NERF_PE_SEPARATE   // (A/B build: layer 0 and the skip PE columns as two K = 63 launches)
-  if ((rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
-#endif
+  // layer 0 and the skip layer's PE columns (both over enc_x): one launch of the split arithmetic's
+  // pair kernel; under f32 two K = 63 jobs on the f32 GEMM like every other weight gradient
+  const bool pe_pair = g_mlp_arith == NERF_ARITH_F16X3;
+  if (pe_pair && (rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
   for (const Job& j : jobs) {
-#ifndef NERF_PE_SEPARATE
-    if (j.K == kPosEnc) continue;            // (in the pair above)
-#endif
+    if (pe_pair && j.K == kPosEnc) continue;            // (in the pair above)
     if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
-#ifndef NERF_HEAD3_GEMM   // (A/B build: the rgb head on the 128 x 128 tile GEMM)
     if (j.a == kGradRgb) {   // the rgb head: the streaming kernel (3 rows)
       if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
                                    j.b ? wb : wa, wfl, j.b ? sb : sa)))
         return rc;
       continue;
     }
-#endif
     const H16Meta hm = block_exps(save, grad, j.ja, j.jx);
     if ((rc = launch_wgrad(grad + tile_col(j.a), kGradRow, j.n, save + tile_col(j.x), kSaveRow, j.K, 1, M, g[j.p] + j.k0,
                            j.ldo, j.bias ? g[j.p + 1] : nullptr, 0, j.b ? wb : wa, j.b ? sb : sa, nullptr, true, true,
@@ -3516,21 +2871,13 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
 static int param_grads(const float* save, const float* grad, int64_t M, int N, const float* app, int64_t app_rows,
                        const float* packed, float* const* g, float* dapp, float* ws, size_t ws_floats,
                        hipStream_t s) {
-#ifndef NERF_NO_RAYSUM   // (A/B build: NERF_NO_RAYSUM keeps the M-row GEMMs for every N)
   const bool ray_path = N >= kRaySumMinN;
-#else
-  const bool ray_path = false;
-#endif
   const size_t rf = ray_path ? ray_sum_floats(M) : 0;
   if (ws_floats < rf + 64) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
   const size_t avail = (ws_floats - rf) & ~(size_t)63;   // partial buffers; the ray sums after them, aligned
   float* rays = ray_path ? ws + avail : nullptr;
   const size_t w1 = (wgrad_stream_floats(M) + 63) & ~(size_t)63;
-#ifndef NERF_PG_ONE_STREAM   // (A/B build: every job on the caller's stream)
   const bool two = avail >= 2 * w1;
-#else
-  const bool two = false;
-#endif
   if (!two) return param_grads_jobs(save, grad, M, N, app, app_rows, packed, g, dapp, ws, ws, avail, rays, s, s);
   PgStreams* ps;
   int rc;

@@ -15,7 +15,6 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
   case $step in
-    variants) run variants 300 python scripts/mlp_variants.py ;;
     pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
     pytest_all) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     pytest_new) run pytest_new 900 python -u -m pytest tests/test_gpu_autograd.py tests/test_gpu_shards.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;

@@ -1,12 +1,12 @@
 """The build-time ISA guard (scripts/check_isa.py, `make check-isa`, run by __graft_entry__.build()).
 
-M0: the LDS-DMA weight streams of mlp16_kernel and mlp_backward16_lds_kernel declare M0 clobbered, so
+M0: the LDS-DMA weight streams of mlp16_kernel and mlp_backward16_bound_kernel declare M0 clobbered, so
 nothing else in those kernels may read M0.  The check passes on the shipped libnerfmi.so and fails on
 the same disassembly with an M0 reader inserted (explicit operand, implicit reader, a write the DMA does
 not consume).
 
 vmcnt: every publish of an LDS-DMA ring (the counted `s_waitcnt vmcnt(N)` + `s_barrier` of
-stream16.h, train.hip's bw_publish) must leave in flight only pieces younger
+stream16.h, shared by the forward and the data gradient) must leave in flight only pieces younger
 than the published chunk, on every path of the kernel's control-flow graph.  Shown on the shipped
 library (passes), on the shipped disassembly with one publish over-counted, a flat op in the window
 or the exit drain removed (fails), and on committed disassemblies of three builds
@@ -91,7 +91,7 @@ def disasm():
 def test_shipped_library_is_clean(disasm):
     report, checked = check_isa.check(disasm)
     assert any("mlp16_kernel<false>" in n for n in checked) and any("mlp16_kernel<true>" in n for n in checked)
-    assert any("mlp_backward16_lds_kernel" in n for n in checked)
+    assert any("mlp_backward16_bound_kernel" in n for n in checked)
     assert report == {}, report
 
 
@@ -111,7 +111,7 @@ def _insert(text, kernel, line, after=5):
     return "\n".join(out)
 
 
-@pytest.mark.parametrize("kernel", ["mlp16_kernel<false>", "mlp_backward16_lds_kernel"])
+@pytest.mark.parametrize("kernel", ["mlp16_kernel<false>", "mlp_backward16_bound_kernel"])
 @pytest.mark.parametrize("line", ["s_movrel_b32 s0, s1", "ds_read_addtid_b32 v0", "s_mov_b32 s3, m0",
                                   "s_mov_b32 m0, 0x100", "v_readfirstlane_b32 s2, v1 ; s_add_u32 s2, s2, m0"])
 def test_inserted_m0_reader_is_caught(disasm, kernel, line):
@@ -133,7 +133,7 @@ def test_unconsumed_m0_write_is_caught(disasm):
 # ---- counted vmcnt waits of the LDS-DMA streams (check_isa.check_vmcnt) ---------------------------
 def test_stream_kernels_are_checked(disasm):
     report, checked = check_isa.check(disasm)
-    for k in ("mlp16_kernel<true>", "mlp16_kernel<false>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel"):
+    for k in ("mlp16_kernel<true>", "mlp16_kernel<false>", "mlp_backward16_bound_kernel"):
         assert any(k in n for n in checked), k
     assert report == {}, report
 
@@ -156,7 +156,7 @@ def _publish_waits(text, kernel):
     return lines, out
 
 
-@pytest.mark.parametrize("kernel", ["mlp16_kernel<true>", "mlp_backward16_bound_kernel", "mlp_backward16_lds_kernel"])
+@pytest.mark.parametrize("kernel", ["mlp16_kernel<true>", "mlp_backward16_bound_kernel"])
 def test_overcounted_publish_wait_is_caught(disasm, kernel):
     """One publish wait counting one op more than issued after its chunk's pieces, in the ISA text."""
     lines, waits = _publish_waits(disasm, kernel)
