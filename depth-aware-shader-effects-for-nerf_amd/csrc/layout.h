@@ -222,13 +222,14 @@ NERF_HD constexpr int64_t tile_col(int c) { return (int64_t)(c / 8) * 256; }
 NERF_HD constexpr int64_t tile_off(int64_t m, int f, int R) {
   return (m / 32) * 32 * (int64_t)R + (int64_t)(f / 8) * 256 + (m % 32) * 8 + f % 8;
 }
-// Block exponents (the split arithmetic's weight gradient, train.hip wgrad_h16w_kernel).  The
-// f16x3 forward and data-gradient kernels record, for each 32-sample block and each 256-wide
-// weight-gradient operand, the exponent e of the block's largest |value| (max < 2^e; an all-zero
-// block e = kBlockExpZero), as the integer-valued float -(kBlockExpBias + e), in row padding:
-//   save rows: entry j (j < 8: h_j) in enc_x's pad slot (feature kSaveEncX + 63) of sample j;
-//   gradient rows: entry j (j < 7: dpre_{j+1}; j = 7: [dpre_dir | dsigma_pre]) in the first pad
-//   float after dsigma_pre (feature kGradSigma + 1) of sample j.
+// Block exponents (the split arithmetic's weight gradients, train.hip wgrad_h16h_kernel and
+// wgrad_pair16_kernel).  The f16x3 forward and data-gradient kernels record, for each 32-sample block
+// and each weight-gradient operand, the exponent e of the block's largest |value| (max < 2^e; an
+// all-zero block e = kBlockExpZero), as the integer-valued float -(kBlockExpBias + e), in row padding:
+//   save rows: entry j (j < 8: h_j; j = 8: enc_x) in enc_x's pad slot (feature kSaveEncX + 63) of
+//   sample j;
+//   gradient rows: entry j (j < 7: dpre_{j+1}; j = 7: [dpre_dir | dsigma_pre]; j = 8: dpre_0) in the
+//   first pad float after dsigma_pre (feature kGradSigma + 1) of sample j.
 // Every other writer leaves those slots 0 (the f32 forward's zero pad, the other backward kernels),
 // which reads as "absent": the GEMM then finds the chunk's maximum itself.
 constexpr int kMetaSaveF = kSaveEncX + 63;

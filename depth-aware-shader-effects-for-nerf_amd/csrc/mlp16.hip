@@ -261,6 +261,13 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 #pragma unroll
   for (int p = 0; p < kPeSteps; ++p) pe_mine[p * 64 + lane] = pe[p];
   const float m_pe = fmaxf(1.0f, fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2]))));   // bounds |PE|
+  float rec_encx = 0.0f;    // training: the block exponent record of enc_x (entry 8, layout.h)
+  if constexpr (SAVE) {
+    float mx = 0.0f;
+#pragma unroll
+    for (int p = 0; p < kPeSteps; ++p) mx = fmaxf(mx, fabsf(pe[p]));
+    rec_encx = block_exp_record(wave_max_nn(sample_max(mx)));
+  }
 
   const float* bias = lds + kLdsBias;
   const float* ws = lds + kLdsSigmaW;
@@ -282,7 +289,8 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
 
   f32x16 acc[8];
   float m = 0.0f, part = 0.0f;
-  float bexp = 0.0f;   // training: lane j < 8 gathers the block exponent record of h_j (layout.h)
+  // training: lane j < 8 gathers the block exponent record of h_j, lane 8 holds enc_x's (layout.h)
+  float bexp = (lane & 31) == 8 ? rec_encx : 0.0f;
   float inv_cur = cst[kS16InvW + 0] / s_cur;                // exact: powers of two
   float s_nxt = pow2_scale(cst[kS16R + 0] * m_pe + cst[kS16B + 0]);
   STAMP16(1);
@@ -499,7 +507,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   }
   if constexpr (SAVE) {
     if (valid) {   // enc_x in the reference order (pe_feature; slot 63: the block exponents, layout.h), enc_d
-      const float pad = (lane & 31) < 8 ? bexp : 0.0f;
+      const float pad = (lane & 31) < 9 ? bexp : 0.0f;
 #pragma unroll
       for (int p = 0; p < kPeSteps; ++p) {
         const int f = pe_feature(p, h);

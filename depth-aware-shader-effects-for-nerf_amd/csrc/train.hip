@@ -841,10 +841,8 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
     if constexpr (SIGMA) x = fmaf(dsp, qv.w[e], x);
     const float d = (qv.mw >> (SH + e)) & 1u ? x : 0.0f;
     dv[e] = d;
-    if constexpr (SPLIT) {
-      m = fmaxf(m, fabsf(d));
-      xs[e] = d * s;
-    }
+    m = fmaxf(m, fabsf(d));          // (layer 0, SPLIT = false: its block exponent record)
+    if constexpr (SPLIT) xs[e] = d * s;
   }
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
                                          (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice),
@@ -1090,9 +1088,14 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
     bw_quarter<0, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
     bw_quarter<1, 4, 8, QG, false, false>(acc, inv_prev, 0.0f, wsig, h, 0.0f, in, m, qv[0], g_prev);
   });
+  {   // m = the sample's max |d pre_0| (tiles 0-3 from layer 1's group B, 4-7 above): entry 8, read by
+      // the split-f16 layer-0 / skip-PE pair (wgrad_pair16_kernel)
+    const float rec = block_exp_record(wave_max_nn(sample_max(m)));
+    bexp = (lane & 31) == 8 ? rec : bexp;
+  }
   // the records: sample j's feature kMetaGradF (lane half 1 writes a 0 four pad floats on; tail lanes'
   // offsets lie outside the buffer range)
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h == 0 && (lane & 31) < 8 ? bexp : 0.0f), ga.rows,
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h == 0 && (lane & 31) < 9 ? bexp : 0.0f), ga.rows,
                                         (int)ga.loff + 4 * (int)(tile_col(kMetaGradF) + kMetaGradF % 8), 0, 0);
 }
 
@@ -1888,10 +1891,16 @@ wgrad_h16w_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
 // output rows from nrows on are not stored; the partial has nrows rows (wgrad_stride(nrows, 256)).
 // The bias column: each a column has two threads (samples 0-7 and 8-15 of every stage), each summing
 // in double; their sums are added once at the end (wgrad_h16w_kernel: one thread, all 16).
-template <int NS>
+// SUMS (the dir/density launch, rays of N % 32 == 0 samples): the threads of a columns 0..127
+// (d pre_dir) also write each stage's sum of their 8 raw values (in double, rounded once) to
+// sums[(m / 8) * 128 + column], m the first of the 8 samples: the per-ray inputs' GEMMs (dir_linear's
+// PE_4(d) columns) then run over M / 8 rows of these sums instead of re-reading the gradient rows
+// (ray_sums_kernel's 256 columns per sample).
+template <int NS, bool SUMS = false>
 __global__ void __launch_bounds__(256, 2)
 wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int64_t M,
-                  int clen, int chunks, int nrows, H16Meta meta, float* __restrict__ partial) {
+                  int clen, int chunks, int nrows, H16Meta meta, float* __restrict__ partial,
+                  float* __restrict__ sums = nullptr) {
   __shared__ __attribute__((aligned(16))) _Float16 As[2][2][128][kBfRow];   // [buffer][hi, lo][column][sample]
   __shared__ float wmax[4][2];
   __shared__ double bsum[128];
@@ -1937,10 +1946,21 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   int Ea, Ex;
   h16_chunk_exps<true>(a, lda, x, ldx, M, m0, m1, meta, wmax, Ea, Ex);
   const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
-  auto split_a = [&](auto set_c, int buf) __attribute__((always_inline)) {
+  __amdgpu_buffer_rsrc_t sres;   // SUMS: this chunk's rows of 8-sample sums (half 0 only)
+  if constexpr (SUMS)
+    sres = __builtin_amdgcn_make_buffer_rsrc(sums + (m0 / 8) * kDirHidden, (short)0,
+                                             half == 0 ? (int)(mrel_end / 8 * kDirHidden * 4) : 0, 0x00020000);
+  auto split_a = [&](auto set_c, int buf, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
+    double ps = 0.0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
+    for (int j = 0; j < 8; ++j) ps += (double)ra[SET][j];
+    bacc += ps;
+    // float (m0 + 16 stage + as0) / 8 * 128 + (tid & 127) = (m0 / 8 + 2 stage) 128 + tid; past the
+    // chunk (and in the half-1 workgroups) the store falls outside the resource and is dropped
+    if constexpr (SUMS)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)ps), sres, 4 * tid, 2 * kDirHidden * 4 * stage,
+                                            kRowStoreAux);
     h16x8 hi, lo;
     split2_f16(ra[SET], sa, hi, lo);
     *reinterpret_cast<h16x8*>(&As[buf][0][tid & 127][as0]) = hi;
@@ -1954,7 +1974,7 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   load(std::integral_constant<int, 0>{}, 0);
   if constexpr (NS > 2) load(std::integral_constant<int, (NS > 2 ? 1 : 0)>{}, 1);
   if constexpr (NS > 3) load(std::integral_constant<int, (NS > 3 ? 2 : 0)>{}, 2);
-  split_a(std::integral_constant<int, 0>{}, 0);
+  split_a(std::integral_constant<int, 0>{}, 0, 0);
   __syncthreads();
   // iteration st (IT = st mod U: set IT % NS, buffer IT % 2): stage st+NS-1's loads; stage st's x
   // split and MFMAs, stage st+1's a split in their shadow; barrier
@@ -1986,7 +2006,7 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
         acc[i][j] = mfma16(f[0], fx[j][0], t);
       }
     }
-    split_a(Nxt{}, FB ^ 1);
+    split_a(Nxt{}, FB ^ 1, st + 1);
     __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);        // the x split
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);         // tile 0's reads
 #pragma unroll
@@ -2037,14 +2057,13 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
 // registers, so two workgroups share a CU and keep more loads in flight (1 KiB of a + 252 B of x
 // per sample).  Loads run two stages ahead, unconditionally.  75 us per 262K-sample launch against
 // 105 us on 256 x 64 tiles of wgrad_bf_kernel (scripts/wgrad_libs_trace.sh, K=63).
-// NW = 16 (DUAL): two 256-row gradients over the same x in one launch, rows 256.. from a2 (layer 0's
-// d pre_0 and the skip layer's d pre_4, both over enc_x: x is read once, and 16 waves per workgroup
-// keep twice the loads in flight): 512 x K partials, each thread loading one x sample per stage.
-template <bool BLK, int NW = 8>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
-__global__ void __launch_bounds__(64 * NW)
+// (The split arithmetic's layer-0 / skip-PE pair runs wgrad_pair16_kernel below: this kernel serves
+// nerf_wgrad's 256 x (K <= 64) GEMMs under f16x3.)
+template <bool BLK>   // BLK: a and x tile-major (layout.h; see wgrad_bf_kernel)
+__global__ void __launch_bounds__(512)
 wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ x, int64_t ldx, int K,
-                    int64_t M, int clen, float* __restrict__ partial, const float* __restrict__ a2 = nullptr) {
-  static_assert(NW == 8 || NW == 16, "one or two 256-row gradients");
+                    int64_t M, int clen, float* __restrict__ partial) {
+  constexpr int NW = 8;
   constexpr int XS = 16 / NW;        // x samples per thread and stage
   __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][64][kBfRow];
   const int chunk = blockIdx.x;
@@ -2053,7 +2072,6 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = lane >> 5, c = lane & 31;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
-  if (NW == 16 && w >= 8) a = a2;    // (wave-uniform)
   const int ac = 32 * (w & 7) + c;
   const uint32_t avo = BLK ? 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h) : (uint32_t)(8 * h) * lda4 + 4u * (uint32_t)ac;
   const uint32_t as4 = BLK ? 32u : lda4, xs4 = BLK ? 32u : ldx4;   // byte step from sample j to j + 1
@@ -2159,6 +2177,170 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
   // bias column: this lane summed column 32w + c over its 8 samples of every stage
   bacc += __shfl_xor(bacc, 32);
   if (h == 0) out[(size_t)(32 * w + c) * KP + K] = (float)bacc;
+}
+
+// Layer 0's weight gradient (d pre_0 over enc_x) and the skip layer's PE columns (d pre_4 over enc_x)
+// of the split arithmetic as one 512 x 63 GEMM on split-f16 MFMA (wgrad_bf_k64_kernel<true, 16>'s
+// shape with wgrad_h16h_kernel's arithmetic: three f16 products per fp32 product instead of bf16x6's
+// six, two f16 parts to split instead of three bf16 parts).  16 waves per 1,024-sample chunk: wave w
+// owns output rows 32w .. 32w+31 (waves 0-7 of d pre_0, 8-15 of d pre_4; one MFMA row tile, two
+// column tiles), loads its a columns straight in A-fragment order and splits them in registers; x =
+// enc_x (63 columns + the pad slot, which is never read) is split once per workgroup into LDS, one
+// sample of one column per thread and stage.  enc_x is read once for both gradients.
+// Scales: one power of two per chunk and operand, s = 2^(14 - e) (h16_chunk_exps), from the producers'
+// block exponent records (layout.h: d pre_0 = gradient entry 8, d pre_4 = entry 3, enc_x = save entry
+// 8), else from a pass over the chunk (workgroup-uniform branch).  The two halves' a scales differ, so
+// each wave unscales its 32 accumulators itself (exact: powers of two) and the partial is plain fp32
+// (wgrad_reduce_kernel, scaled = 0).  The bias column sums the raw a values in double.
+constexpr int kPairWaves = 16;
+__global__ void __launch_bounds__(64 * kPairWaves)
+wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ save, int64_t M, int clen,
+                    float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][64][kBfRow];   // [buffer][hi, lo][column][sample]
+  __shared__ float wmax[kPairWaves][2];
+  const int chunk = blockIdx.x;
+  const int64_t m0 = (int64_t)chunk * clen;
+  const int64_t m1 = m0 + clen < M ? m0 + clen : M;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, c = lane & 31, half = w >> 3;
+  const float* a = grad + tile_col(half ? kSkipLayer * kHidden : 0);     // (wave-uniform)
+  const float* x = save + tile_col(kSaveEncX);
+  constexpr uint32_t lda4 = kGradRow * 4u, ldx4 = kSaveRow * 4u;
+  const int ac = 32 * (w & 7) + c;
+  const uint32_t avo = 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h);   // sample j of the stage at + 32 j bytes
+  const int xc = tid & 63, xp = tid >> 6;                                 // x: column xc, sample xp of a stage
+  const uint32_t xvo = xc < kPosEnc ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 8 * xp) : 0x80000000u;
+  const uint32_t mrel_end = (uint32_t)(m1 - m0);
+
+  // ---- the chunk's exponents: records (every wave reads all three, so the branch is uniform)
+  const int64_t b0 = m0 / 32, nb = (m1 - 1) / 32 - b0 + 1;
+  const float* rec0 = grad + tile_col(kMetaGradF) + kMetaGradF % 8 + 8 * 8;   // entry 8: d pre_0
+  const float* rec4 = grad + tile_col(kMetaGradF) + kMetaGradF % 8 + 8 * 3;   // entry 3: d pre_4
+  const float* recx = save + tile_col(kMetaSaveF) + kMetaSaveF % 8 + 8 * 8;   // entry 8: enc_x
+  float r0 = 0.0f, r4 = 0.0f, rx_ = 0.0f, bad = 0.0f;
+  for (int64_t b = lane; b < nb; b += 64) {
+    const float v0 = rec0[(b0 + b) * 32 * kGradRow], v4 = rec4[(b0 + b) * 32 * kGradRow];
+    const float vx = recx[(b0 + b) * 32 * kSaveRow];
+    bad = (block_exp_valid(v0) && block_exp_valid(v4) && block_exp_valid(vx)) ? bad : 1.0f;
+    r0 = fmaxf(r0, -v0);
+    r4 = fmaxf(r4, -v4);
+    rx_ = fmaxf(rx_, -vx);
+  }
+  int Ea, Ex;
+  if (wave_max_nn(bad) == 0.0f) {
+    Ea = (int)wave_max_nn(half ? r4 : r0) - kBlockExpBias;
+    Ex = (int)wave_max_nn(rx_) - kBlockExpBias;
+  } else {   // absent: the chunk's whole 32-sample blocks read once (the records' span)
+    float ma = 0.0f, mx = 0.0f;
+    const int64_t f0 = b0 * 32, f1 = (b0 + nb) * 32 < M ? (b0 + nb) * 32 : M;
+    for (int64_t ms = f0; ms < f1; ms += kBfStage) {
+      const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(a + (ms / 32) * 32 * kGradRow + (ms % 32) * 8), (short)0, (int)(32 * lda4 - (ms % 32) * 32),
+          0x00020000);
+      const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(x + (ms / 32) * 32 * kSaveRow + (ms % 32) * 8), (short)0, (int)(32 * ldx4 - (ms % 32) * 32),
+          0x00020000);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        ma = fmaxf(ma, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, 0))));
+      mx = fmaxf(mx, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, 0, 0))));
+    }
+    ma = wave_max_nn(ma);
+    mx = wave_max_nn(mx);
+    if (lane == 0) {
+      wmax[w][0] = ma;
+      wmax[w][1] = mx;
+    }
+    __syncthreads();
+    ma = 0.0f;
+    mx = 0.0f;
+    for (int v = 0; v < kPairWaves; ++v) {
+      if ((v >> 3) == half) ma = fmaxf(ma, wmax[v][0]);
+      mx = fmaxf(mx, wmax[v][1]);
+    }
+    Ea = (int)(-block_exp_record(ma)) - kBlockExpBias;
+    Ex = (int)(-block_exp_record(mx)) - kBlockExpBias;
+  }
+  Ea = __builtin_amdgcn_readfirstlane(Ea < kH16EMin ? kH16EMin : Ea);
+  Ex = __builtin_amdgcn_readfirstlane(Ex < kH16EMin ? kH16EMin : Ex);
+  const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
+
+  float ra[2][8], rx[2];
+  double bacc = 0.0;                 // bias column (this lane's column, its 8 samples of every stage)
+  auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const uint32_t rel0 = (uint32_t)(kBfStage * stage) < mrel_end ? (uint32_t)(kBfStage * stage) : mrel_end;
+    const int64_t ms = m0 + rel0;
+    const bool live = rel0 < mrel_end;   // past the chunk: an empty resource, the loads read zeros
+    const __amdgpu_buffer_rsrc_t ares = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a + (ms / 32) * 32 * kGradRow + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * lda4 - (ms % 32) * 32) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + (ms / 32) * 32 * kSaveRow + (ms % 32) * 8), (short)0,
+        live ? (int)(32 * ldx4 - (ms % 32) * 32) : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, kRowLoadAux));
+    rx[SET] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, 0, kRowLoadAux));
+  };
+  auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const float v = rx[SET] * sx;
+    const _Float16 hi = (_Float16)v;
+    Xs[buf][0][xc][xp] = hi;
+    Xs[buf][1][xc][xp] = split_lo(v, hi);
+  };
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  const int nstages = (int)((m1 - m0 + 2 * kBfStage - 1) / (2 * kBfStage)) * 2;   // even; the extra reads zeros
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(S0{}, 0);
+  load(S1{}, 1);
+  store_x(S0{}, 0);
+  __syncthreads();
+  // iteration st: split stage st's a (set st % 2) in registers, reuse the set for stage st+2's loads,
+  // stage st's MFMAs (x from LDS buffer st % 2), stage st+1's x into the other buffer
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    using Other = std::integral_constant<int, 1 - SET>;
+    const int buf = SET;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
+    h16x8 fh, fl;
+    split2_f16(ra[SET], sa, fh, fl);
+    load(set_c, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const h16x8 xh = *reinterpret_cast<const h16x8*>(&Xs[buf][0][32 * t + c][8 * h]);
+      const h16x8 xl = *reinterpret_cast<const h16x8*>(&Xs[buf][1][32 * t + c][8 * h]);
+      f32x16 v = mfma16(fl, xh, acc[t]);   // small products first
+      v = mfma16(fh, xl, v);
+      acc[t] = mfma16(fh, xh, v);
+    }
+    store_x(Other{}, buf ^ 1);   // (after the last stage: zeros into the idle buffer)
+    __syncthreads();
+  };
+  for (int st = 0; st < nstages; st += 2) {
+    iteration(S0{}, st);
+    iteration(S1{}, st + 1);
+  }
+  // acc = sum (a 2^(14-Ea)) (x 2^(14-Ex)): unscaled here by two exact power-of-two factors (each
+  // normal for any exponent the clamps allow)
+  const int e = Ea + Ex - 28;
+  const float u0 = ldexpf(1.0f, e / 2), u1 = ldexpf(1.0f, e - e / 2);
+  constexpr int KP = kPosEnc + 1;
+  float* out = partial + (size_t)chunk * wgrad_stride(2 * kHidden, kPosEnc);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kk = 32 * t + c;
+    if (kk < kPosEnc) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) out[(size_t)(32 * w + (g & 3) + 8 * (g >> 2) + 4 * h) * KP + kk] = (acc[t][g] * u0) * u1;
+    }
+  }
+  bacc += __shfl_xor(bacc, 32);
+  if (h == 0) out[(size_t)(32 * w + c) * KP + kPosEnc] = (float)bacc;
 }
 
 // The rgb head's weight gradient (rgb_linear: 3 rows over hd, K = 128) on tile-major rows: a
@@ -2390,7 +2572,7 @@ static int launch_wgrad_head3(const float* a, const float* x, int64_t M, float* 
 }
 
 // Layer 0's weight gradient (d pre_0 over enc_x) and the skip layer's PE columns (d pre_4 over
-// enc_x) as one 512 x 63 GEMM over the tile-major rows (wgrad_bf_k64_kernel<NW = 16>): enc_x is read
+// enc_x) as one 512 x 63 split-f16 GEMM over the tile-major rows (wgrad_pair16_kernel): enc_x is read
 // once; rows 0..255 go to layer 0's weight + bias, rows 256.. to the skip weight's PE columns.
 static int launch_wgrad_pe_pair(const float* save, const float* grad, int64_t M, float* w0, float* b0, float* w4,
                                 float* ws, size_t ws_floats, hipStream_t s) {
@@ -2399,9 +2581,8 @@ static int launch_wgrad_pe_pair(const float* save, const float* grad, int64_t M,
   const int chunks = (int)((M + clen - 1) / clen);
   if ((size_t)chunks * wgrad_stride(2 * kHidden, kPosEnc) > ws_floats)
     return set_error(NERF_ERR_WORKSPACE, "wgrad pe pair: workspace");
-  hipLaunchKernelGGL((wgrad_bf_k64_kernel<true, 16>), dim3((unsigned)chunks), dim3(1024), 0, s, grad + tile_col(0), kGradRow,
-                     save + tile_col(kSaveEncX), kSaveRow, kPosEnc, M, clen, ws, grad + tile_col(4 * kHidden));
-  if (int rc = check_launch("wgrad_bf_k64_kernel<16>")) return rc;
+  hipLaunchKernelGGL(wgrad_pair16_kernel, dim3((unsigned)chunks), dim3(64 * kPairWaves), 0, s, grad, save, M, clen, ws);
+  if (int rc = check_launch("wgrad_pair16_kernel")) return rc;
   const WgradSplit skip{kHidden, w4 + kHidden, kHidden + kPosEnc, kPosEnc, nullptr};
   const int64_t cols4 = wgrad_stride(2 * kHidden, kPosEnc) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks,
@@ -2416,7 +2597,7 @@ static int launch_wgrad_pe_pair(const float* save, const float* grad, int64_t M,
 int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx, int K, int64_t x_div, int64_t M,
                  float* out_w, int ldo, float* out_b, int accumulate, float* ws, hipStream_t s,
                  const WgradSplit* split = nullptr, bool tiled = false, bool x_tiled = true,
-                 const H16Meta* meta = nullptr) {
+                 const H16Meta* meta = nullptr, float* sums = nullptr) {
   const H16Meta hm = meta ? *meta : H16Meta{};
   if (M == 0) return NERF_OK;
   const int KP = K + 1;
@@ -2426,6 +2607,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     return set_error(NERF_ERR_BAD_ARG, "wgrad: tile-major operands must be aligned with row lengths % 8 == 0");
   const bool x_blk = tiled && x_tiled && x_div == 1;   // x tile-major
   int rc;
+  bool sums_done = false;                               // (sums: written by the h16h launch only)
   bool scaled = false;                                  // partials of wgrad_h16w_kernel (chunk exponents)
   // the split arithmetic (buffer offsets of a chunk's rows must stay below 2^31): the whole-tile
   // GEMMs on split-f16 MFMA, the rest on bf16x6
@@ -2435,10 +2617,15 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     if (wgrad_whole_tile(N, K) && x_div == 1 && tiled && x_blk) {
       // tile-major rows (the training path): two workgroups per CU, half the rows each; the
       // dir_linear + density launch (N = 160) keeps 160 of 256 rows
-      hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx, M,
-                         clen, chunks, N, hm, ws);
+      if (sums)   // (the dir/density launch also writes d pre_dir's 8-sample sums, wgrad_h16h_kernel)
+        hipLaunchKernelGGL((wgrad_h16h_kernel<3, true>), dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda,
+                           x, ldx, M, clen, chunks, N, hm, ws, sums);
+      else
+        hipLaunchKernelGGL(wgrad_h16h_kernel<3>, dim3((unsigned)((chunks + 7) / 8 * 16)), dim3(256), 0, s, a, lda, x, ldx,
+                           M, clen, chunks, N, hm, ws, nullptr);
       rc = check_launch("wgrad_h16h_kernel");
       scaled = true;
+      sums_done = true;
     } else if (N == kWT && wgrad_whole_tile(N, K) && x_div == 1 && !tiled) {   // nerf_wgrad's row-major operands
       hipLaunchKernelGGL(wgrad_h16w_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, lda, x, ldx, M, clen, hm, ws);
       rc = check_launch("wgrad_h16w_kernel");
@@ -2471,6 +2658,7 @@ int launch_wgrad(const float* a, int64_t lda, int N, const float* x, int64_t ldx
     rc = check_launch("wgrad_kernel");
   }
   if (rc) return rc;
+  if (sums && !sums_done) return set_error(NERF_ERR_BAD_ARG, "wgrad: 8-sample sums need the split-f16 whole-tile launch");
   const int64_t cols4 = wgrad_stride(N, K) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks, N, K,
                      out_w, ldo, out_b, accumulate, split ? *split : WgradSplit{}, (int)scaled);
@@ -2530,9 +2718,38 @@ ray_sums_kernel(const float* __restrict__ grad, const float* __restrict__ save, 
   if (t < 32) E[r * 32 + t] = save[tile_off(m0, kSaveEncD + t, kSaveRow)];
 }
 
-// Floats of the ray-sum buffers (S, E) for any N >= kRaySumMinN: B = M / N <= M / kRaySumMinN rays.
+// Rays of N % 32 == 0 samples under the split arithmetic (the fused per-ray sums; the dir/density
+// launch writes d pre_dir's 8-sample sums, wgrad_h16h_kernel SUMS): per 32-sample block b (all on one
+// ray), S_hd[b] = the block's sum of d hd = W_rgb^T (the sum of its 32 d rgb_pre rows) (models.py:
+// 154-160: d hd = W_rgb^T d rgb_pre is linear in the sample, so the block sum needs the 3 column
+// sums; in double, rounded once), and for a ray's first block E[ray] = the ray's PE_4(d) (its first
+// sample's save row).  Reads 1 KiB of gradient rows per block instead of ray_sums_kernel's 256
+// columns per sample.
+__global__ void __launch_bounds__(128)
+block_head_sums_kernel(const float* __restrict__ grad, const float* __restrict__ save, const float* __restrict__ packed,
+                       int N, float* __restrict__ S_hd, float* __restrict__ E) {
+  __shared__ double dsum[3];
+  const int64_t b = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t < 3) {   // the block's 32 d rgb_pre of column t, in sample order
+    double acc = 0.0;
+    for (int j = 0; j < 32; ++j) acc += (double)grad[tile_off(b * 32 + j, kGradRgb + t, kGradRow)];
+    dsum[t] = acc;
+  }
+  __syncthreads();
+  const float* W = packed + kOffRgbW;   // rgb_linear.weight (3 x 128)
+  S_hd[b * kDirHidden + t] =
+      (float)(dsum[0] * (double)W[t] + dsum[1] * (double)W[kDirHidden + t] + dsum[2] * (double)W[2 * kDirHidden + t]);
+  if ((b * 32) % N == 0 && t < 32) E[(b * 32 / N) * 32 + t] = save[tile_off(b * 32, kSaveEncD + t, kSaveRow)];
+}
+
+// The ray-sum buffers for any N >= kRaySumMinN (B = M / N <= M / kRaySumMinN rays): region A holds
+// S (B x 256, ray_sums_kernel) or the fused path's 8-sample sums of d pre_dir ((M / 8) x 128), region
+// B the fused path's S_hd ((M / 32) x 128), region C E (B x 32).
 constexpr int kRaySumMinN = 32;
-static size_t ray_sum_floats(int64_t M) { return (size_t)(M / kRaySumMinN + 1) * (256 + 32) + 64; }
+static size_t ray_sum_a_floats(int64_t M) { return (size_t)(M / 8 + 1) * kDirHidden; }   // >= (M / 32 + 1) 256
+static size_t ray_sum_b_floats(int64_t M) { return (size_t)(M / 32 + 1) * kDirHidden; }
+static size_t ray_sum_floats(int64_t M) { return ray_sum_a_floats(M) + ray_sum_b_floats(M) + (size_t)(M / 32 + 1) * 32 + 64; }
 
 // ------------------------------------------------------------------------------------ Adam
 // torch.optim.Adam (amsgrad=False, maximize=False, weight_decay=0) element for element:
@@ -2820,19 +3037,44 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     // one 160 x 256 GEMM on the whole-tile kernel (5 row tiles) over a = the gradient columns from
     // d pre_dir on ([d pre_dir | d sigma | pad | d hd...]) and x = h7: rows 0..127 are dir_linear's
     // gradient (+ its bias column), row 128 the density head's, rows 129.. are dropped (h7 is read once).
-    // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over the
-    // B rays of the per-ray gradient sums (ray_sums_kernel), which replace two M-row GEMMs.
+    // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over
+    // per-ray (or per-block) gradient sums, which replace two M-row GEMMs: under the split arithmetic
+    // with N % 32 == 0 the dir/density launch itself writes d pre_dir's 8-sample sums and
+    // block_head_sums_kernel d hd's block sums from d rgb_pre; otherwise ray_sums_kernel reads the
+    // 256 gradient columns of every sample.
     const int64_t B = M / N;
-    float* S = rays;                                       // B x 256
-    float* E = S + (size_t)B * 256;                        // B x 32
+    float* S = rays;                                       // B x 256 (fused: S8, (M / 8) x 128)
+    float* S_hd = S + ray_sum_a_floats(M);                 // fused: (M / 32) x 128
+    float* E = S_hd + ray_sum_b_floats(M);                 // B x 32
     constexpr int kDirRows = 160;
     if (wgrad_workspace_floats(M, kDirRows, kWT) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
     H16Meta hm = block_exps(save, grad, 7, 7);
     hm.a_cols = kDirHidden + 1;                            // d pre_dir, d sigma (rows 129.. are dropped)
+    // fused: the split arithmetic's dir/density launch (wgrad_h16h_kernel) writes d pre_dir's 8-sample
+    // sums, and blocks of 32 samples lie on one ray
+    const bool fused = g_mlp_arith == NERF_ARITH_F16X3 && N % 32 == 0;
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
-                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm)))
+                           M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm,
+                           fused ? S : nullptr)))
       return rc;
+    if (fused) {
+      hipLaunchKernelGGL(block_head_sums_kernel, dim3((unsigned)(M / 32)), dim3(kDirHidden), 0, sb, grad, save, packed, N,
+                         S_hd, E);
+      if ((rc = check_launch("block_head_sums_kernel"))) return rc;
+      // dir_linear's PE_4(d) columns over the M / 8 rows of 8-sample sums (row m: samples 8m .. 8m+7,
+      // ray 8m / N)
+      if ((rc = launch_wgrad(S, kDirHidden, kDirHidden, E, 32, kDirEnc, N / 8, M / 8, g[P_DIR_W] + kHidden,
+                             kHidden + kDirEnc, nullptr, 0, wb, sb)))
+        return rc;
+      if (app_rows == 0) return NERF_OK;     // no appearance: the projection is unused (models.py:146)
+      if ((rc = launch_wgrad(S_hd, kDirHidden, kDirHidden, app, kAppDim, kAppDim, app_rows == 1 ? 0 : N / 32, M / 32,
+                             g[P_APP_W], kAppDim, g[P_APP_B], 0, wb, sb)))
+        return rc;
+      if (!dapp) return NERF_OK;
+      if (app_rows == 1) return launch_app_grad(g[P_APP_B], 1, 1, 1, packed, dapp, sb, false);
+      return launch_app_grad(S_hd, kDirHidden, app_rows, N / 32, packed, dapp, sb, false);
+    }
     hipLaunchKernelGGL(ray_sums_kernel, dim3((unsigned)B), dim3(256), 0, sb, grad, save, N, S, E);
     if ((rc = check_launch("ray_sums_kernel"))) return rc;
     if ((rc = launch_wgrad(S, 256, kDirHidden, E, 32, kDirEnc, 1, B, g[P_DIR_W] + kHidden, kHidden + kDirEnc, nullptr,

@@ -33,8 +33,9 @@ extern "C" {
  * of M samples holds NERF_TILE_ROWS(M) rows (the last block whole; its rows past M are zero). */
 #define NERF_TILE_ROWS(M) ((((M) + 31) / 32) * 32)
 /* Block exponents (ABI 11, f16x3 only): sample j of each 32-sample block carries, in enc_x's pad
- * slot (save feature 1087) the exponent record of h_j (j < 8), and in the float after dsigma
- * (gradient feature 2177) that of dpre_{j+1} (j < 7) or [dpre_dir | dsigma] (j = 7): -(1000 + e)
+ * slot (save feature 1087) the exponent record of h_j (j < 8) or enc_x (j = 8), and in the float after
+ * dsigma (gradient feature 2177) that of dpre_{j+1} (j < 7), [dpre_dir | dsigma] (j = 7) or dpre_0
+ * (j = 8): -(1000 + e)
  * with e = frexp's exponent of the block's largest |value| (-126 for an all-zero block); 0 = absent.
  * nerf_param_grads' split-f16 weight gradient scales each chunk from them (csrc/layout.h). */
 /* ReLU masks the f16x3 training forward writes for the backward (uint32 words per sample):

@@ -4,7 +4,7 @@
 O=gpurun_out/r06/a
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread \
-  -k "flips or matches_autograd or small_rows or pe_columns or over_steps or production_batch" > $O/pytest_train.log 2>&1
+  -k "flips or matches_autograd or small_rows or pe_columns or over_steps or production_batch or records or saves_are or ray_path" > $O/pytest_train.log 2>&1
 rc=$?; echo "train tests rc=$rc"; tail -3 $O/pytest_train.log
 [ $rc -ge 124 ] && exit $rc
 bash scripts/gpu_check.sh pytest_all || exit $?

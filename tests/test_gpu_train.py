@@ -230,18 +230,19 @@ def _safe_draw(state, app, R, N, seed, rel=1e-5):
     layer's rms) of the kink: there an fp32 evaluation may land on either side (the CPU's and the
     GPU's roundings differ by host), which moves that sample's whole gradient chain and makes a
     tensor's error a lottery instead of a measurement."""
-    o, d, z, gr, gs = _draw(4 * R, N, seed)
+    K = 8 * R                       # candidates (a 64-sample ray clears every kink ~1 time in 4)
+    o, d, z, gr, gs = _draw(K, N, seed)
     pts = (o[:, None, :] + d[:, None, :] * z[..., None]).reshape(-1, 3)
-    dexp = d[:, None, :].expand(4 * R, N, 3).reshape(-1, 3)
+    dexp = d[:, None, :].expand(K, N, 3).reshape(-1, 3)
     a = None if app is None else (app.double() if app.dim() == 1 else None)
     pres = []
     with torch.no_grad():
         O.nerf_forward({k: v.double() for k, v in state.items()}, pts.double(), dexp.double(), a, keep=pres)
-    ok = torch.ones(4 * R, dtype=torch.bool)
+    ok = torch.ones(K, dtype=torch.bool)
     for p_ in pres:
-        ok &= ((p_.abs() / p_.pow(2).mean().sqrt()) > rel).reshape(4 * R, -1).all(dim=1)
+        ok &= ((p_.abs() / p_.pow(2).mean().sqrt()) > rel).reshape(K, -1).all(dim=1)
     keep = torch.nonzero(ok)[:, 0][:R]
-    assert keep.numel() == R, f"only {keep.numel()} of {4 * R} rays clear the ReLU kinks"
+    assert keep.numel() == R, f"only {keep.numel()} of {K} rays clear the ReLU kinks"
     samp = (keep[:, None] * N + torch.arange(N)).reshape(-1)
     return o[keep], d[keep], z[keep], gr[samp], gs[samp]
 
@@ -313,9 +314,10 @@ def test_forward_saves_are_the_activations(ref_state, app_vec, with_app, N):
         assert rel_l2(save[:, off:off + 256], h) < 1e-5, l
     enc_x = O.positional_encoding(r["pts"], 10).numpy()
     np.testing.assert_allclose(save[:, 1024:1087], enc_x, rtol=1e-5, atol=2e-6)
-    # enc_x's pad slot: the block exponent records of h_0..h_7 under f16x3 (layout.h), else the zero pad
+    # enc_x's pad slot: the block exponent records of h_0..h_7 and enc_x under f16x3 (layout.h), else
+    # the zero pad
     if _lib().get_mlp_arith() == "f16x3":
-        exp = block_records(save, [slice(o, o + 256) for o in offs])
+        exp = block_records(save, [slice(o, o + 256) for o in offs] + [slice(1024, 1087)])
         np.testing.assert_array_equal(save[:, 1087], exp)
     else:
         assert np.all(save[:, 1087] == 0)
@@ -325,14 +327,14 @@ def test_forward_saves_are_the_activations(ref_state, app_vec, with_app, N):
 
 
 def test_gradient_block_records(ref_state, app_vec):
-    """The f16x3 data-gradient kernel records each block's exponent of d pre_1..7 and [d pre_dir |
-    d sigma] in the gradient rows' padding (layout.h); the activation-mask kernel and the f32 path
-    leave the slots 0 (absent), so the weight gradient finds the maxima itself."""
+    """The f16x3 data-gradient kernel records each block's exponent of d pre_1..7, [d pre_dir |
+    d sigma] and d pre_0 in the gradient rows' padding (layout.h); the activation-mask kernel and the
+    f32 path leave the slots 0 (absent), so the weight gradients find the maxima themselves."""
     r = _mlp_forward_backward(ref_state, app_vec, R=40, N=64)
     grad = r["grad"].numpy()
     slot = 2177
     if _lib().get_mlp_arith() == "f16x3":
-        slices = [slice(256 * (j + 1), 256 * (j + 2)) for j in range(7)] + [slice(2048, 2177)]
+        slices = [slice(256 * (j + 1), 256 * (j + 2)) for j in range(7)] + [slice(2048, 2177), slice(0, 256)]
         np.testing.assert_array_equal(grad[:, slot], block_records(grad, slices))
     else:
         assert np.all(grad[:, slot] == 0)
@@ -631,15 +633,18 @@ def _oracle_grads_f32(state, app, R, N, draw):
     return {k: v.grad.numpy() for k, v in sd.items() if v.grad is not None}
 
 
+@pytest.mark.parametrize("N", [40, 64])
 @pytest.mark.parametrize("app_kind", ["broadcast", "per_ray", "none"])
-def test_param_grads_ray_path(ref_state, app_vec, app_kind):
+def test_param_grads_ray_path(ref_state, app_vec, app_kind, N):
     """nerf_param_grads with N >= 32 samples per ray: the per-ray gradient sums (dir_linear's PE_4(d)
     columns, the appearance projection and the appearance rows as GEMMs over rays), dir/sigma on the
-    whole-tile GEMM, the two-stream schedule.  N = 40 so tile-major blocks straddle rays; against the
-    oracle's float64 autograd, and two calls bit-identical (fixed-order reductions on both streams)."""
+    whole-tile GEMM, the two-stream schedule.  N = 40: tile-major blocks straddle rays (ray_sums_kernel);
+    N = 64 under f16x3: the fused sums (the dir/density launch's 8-sample sums of d pre_dir,
+    block_head_sums_kernel's d hd block sums).  Against the oracle's float64 autograd, and two calls
+    bit-identical (fixed-order reductions on both streams)."""
     L = _lib()
     lib, dev = L.load(), L.device()
-    R, N = 48, 40
+    R = 48
     app = {"broadcast": app_vec, "per_ray": torch.randn(R, 32, generator=torch.Generator().manual_seed(5)),
            "none": None}[app_kind]
     draw = _safe_draw(ref_state, app, R, N, seed=3)
