@@ -180,6 +180,10 @@ namespace nerf {
 constexpr int kSaveEncX = 4 * kHidden;                       // 1024
 NERF_HD constexpr int save_h(int l) { return l < 4 ? l * kHidden : kSaveEncX + 64 + (l - 4) * kHidden; }
 constexpr int kSaveEncD = 1088 + 4 * kHidden;                // 2112
+// enc_d is constant along a ray: rays of N >= kEncDPerRayMinN samples carry it in their first
+// sample's row only (the weight gradients read it per ray there, train.hip param_grads); shorter rays
+// in every row (the dir GEMM reads [h7 | enc_d] per sample)
+constexpr int kEncDPerRayMinN = 32;
 constexpr int kSaveRDir = kSaveEncD + 32;                    // 2144
 constexpr int kSaveHd = kSaveRDir + kDirHidden;              // 2272
 constexpr int kSaveRow = kSaveHd + kDirHidden;               // 2400 floats per sample

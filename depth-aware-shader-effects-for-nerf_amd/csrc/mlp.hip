@@ -225,11 +225,13 @@ mlp_kernel(const float* __restrict__ packed, const float* __restrict__ orig, con
         const int F = kSaveEncX + (f < 0 ? kPosEnc : f);
         srow[tile_col(F) + F % 8] = f < 0 ? 0.0f : pe[p];
       }
-      const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
+      if (N < kEncDPerRayMinN || s == r * N) {   // enc_d: per ray (layout.h kEncDPerRayMinN)
+        const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int F = kSaveEncD + 16 * h + 4 * q;
-        *reinterpret_cast<f32x4*>(srow + tile_col(F) + F % 8) = ed[q];
+        for (int q = 0; q < 4; ++q) {
+          const int F = kSaveEncD + 16 * h + 4 * q;
+          *reinterpret_cast<f32x4*>(srow + tile_col(F) + F % 8) = ed[q];
+        }
       }
     }
   }

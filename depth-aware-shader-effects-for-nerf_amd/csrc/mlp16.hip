@@ -516,13 +516,15 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f < 0 ? pad : pe_mine[p * 64 + lane]), wrows,
                                               (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
       }
-      const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
+      if (N < kEncDPerRayMinN || s == r * N) {   // enc_d: per ray (layout.h kEncDPerRayMinN)
+        const f32x4* ed = reinterpret_cast<const f32x4*>(encd + r * 32 + 16 * h);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-      {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
-        const int F = kSaveEncD + 16 * h + 4 * q;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
-                                               (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+        for (int q = 0; q < 4; ++q)
+        {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
+          const int F = kSaveEncD + 16 * h + 4 * q;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
+                                                 (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+        }
       }
     }
   }

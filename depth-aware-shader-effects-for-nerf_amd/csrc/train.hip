@@ -2180,27 +2180,28 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
 }
 
 // Layer 0's weight gradient (d pre_0 over enc_x) and the skip layer's PE columns (d pre_4 over enc_x)
-// of the split arithmetic as one 512 x 63 GEMM on split-f16 MFMA (three f16 products per fp32
-// product, as wgrad_h16h_kernel, instead of bf16x6's six).  16 waves per 1,024-sample chunk: wave w
+// of the split arithmetic as one 512 x 63 GEMM on split-f16 MFMA (wgrad_bf_k64_kernel<true, 16>'s
+// shape with wgrad_h16h_kernel's arithmetic: three f16 products per fp32 product instead of bf16x6's
+// six, two f16 parts to split instead of three bf16 parts).  16 waves per 1,024-sample chunk: wave w
 // owns output rows 32w .. 32w+31 (waves 0-7 of d pre_0, 8-15 of d pre_4; one MFMA row tile, two
-// column tiles).  Every wave loads its own operands straight in fragment order and splits them in
-// registers -- its a columns, and all 64 enc_x columns (63 + the pad slot, which is never read) -- so
-// the waves share no LDS and wait at no barrier: each streams its rows with the next stage's loads in
-// flight while the current stage is split and multiplied, and the 16 waves' reads of one enc_x stage
-// meet in L1/L2 (HBM reads enc_x once for both gradients).  (The first version staged enc_x through
-// LDS with a barrier per 16-sample stage: 274 us per step beside the other stream, against 298 us for
-// the bf16x6 kernel it replaced; profiles/r06/kernel_stats_train_a.csv.)
+// column tiles), loads its a columns straight in A-fragment order and splits them in registers; x =
+// enc_x (63 columns + the pad slot, which is never read) is split once per workgroup into LDS, one
+// sample of one column per thread and stage.  enc_x is read once for both gradients.
 // Scales: one power of two per chunk and operand, s = 2^(14 - e) (h16_chunk_exps), from the producers'
 // block exponent records (layout.h: d pre_0 = gradient entry 8, d pre_4 = entry 3, enc_x = save entry
 // 8), else from a pass over the chunk (workgroup-uniform branch).  The two halves' a scales differ, so
 // each wave unscales its 32 accumulators itself (exact: powers of two) and the partial is plain fp32
 // (wgrad_reduce_kernel, scaled = 0).  The bias column sums the raw a values in double.
-constexpr int kPairWaves = 16, kPairStages = 2;   // (3 stages in flight spill at 16 waves per workgroup)
+// 274 us per step beside the other stream against 298 us for the bf16x6 kernel it replaced; a variant
+// without LDS or barriers (every wave loading and splitting all 64 enc_x columns itself) took 372 us:
+// the 16 waves' dword gathers of x cost more than the per-stage barrier (profiles/r06/
+// kernel_stats_train_a.csv, kernel_stats_train_b.csv).
+constexpr int kPairWaves = 16;
 __global__ void __launch_bounds__(64 * kPairWaves)
 wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ save, int64_t M, int clen,
                     float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) _Float16 Xs[2][2][64][kBfRow];   // [buffer][hi, lo][column][sample]
   __shared__ float wmax[kPairWaves][2];
-  constexpr int NS = kPairStages;
   const int chunk = blockIdx.x;
   const int64_t m0 = (int64_t)chunk * clen;
   const int64_t m1 = m0 + clen < M ? m0 + clen : M;
@@ -2210,15 +2211,9 @@ wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ sa
   const float* x = save + tile_col(kSaveEncX);
   constexpr uint32_t lda4 = kGradRow * 4u, ldx4 = kSaveRow * 4u;
   const int ac = 32 * (w & 7) + c;
-  // lane (c, h): sample j (0..7) of a stage at + 32 j bytes from its offsets; a column ac; x columns
-  // c and 32 + c (63 lies past enc_x: an offset beyond any resource reads 0)
-  const uint32_t avo = 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h);
-  uint32_t xvo[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int xc = 32 * t + c;
-    xvo[t] = xc < kPosEnc ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 64 * h) : 0x80000000u;
-  }
+  const uint32_t avo = 4u * (uint32_t)(tile_col(ac) + ac % 8 + 64 * h);   // sample j of the stage at + 32 j bytes
+  const int xc = tid & 63, xp = tid >> 6;                                 // x: column xc, sample xp of a stage
+  const uint32_t xvo = xc < kPosEnc ? 4u * (uint32_t)(tile_col(xc) + xc % 8 + 8 * xp) : 0x80000000u;
   const uint32_t mrel_end = (uint32_t)(m1 - m0);
 
   // ---- the chunk's exponents: records (every wave reads all three, so the branch is uniform)
@@ -2250,12 +2245,9 @@ wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ sa
           const_cast<float*>(x + (ms / 32) * 32 * kSaveRow + (ms % 32) * 8), (short)0, (int)(32 * ldx4 - (ms % 32) * 32),
           0x00020000);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 8; ++j)
         ma = fmaxf(ma, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, 0))));
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          mx = fmaxf(mx, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], j * 32, 0))));
-      }
+      mx = fmaxf(mx, fabsf(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, 0, 0))));
     }
     ma = wave_max_nn(ma);
     mx = wave_max_nn(mx);
@@ -2277,7 +2269,7 @@ wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ sa
   Ex = __builtin_amdgcn_readfirstlane(Ex < kH16EMin ? kH16EMin : Ex);
   const float sa = ldexpf(1.0f, 14 - Ea), sx = ldexpf(1.0f, 14 - Ex);
 
-  float ra[NS][8], rx[NS][2][8];
+  float ra[2][8], rx[2];
   double bacc = 0.0;                 // bias column (this lane's column, its 8 samples of every stage)
   auto load = [&](auto set_c, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
@@ -2293,39 +2285,49 @@ wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ sa
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       ra[SET][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ares, (int)avo, j * 32, kRowLoadAux));
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        rx[SET][t][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo[t], j * 32, kRowLoadAux));
+    rx[SET] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xres, (int)xvo, 0, kRowLoadAux));
+  };
+  auto store_x = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    const float v = rx[SET] * sx;
+    const _Float16 hi = (_Float16)v;
+    Xs[buf][0][xc][xp] = hi;
+    Xs[buf][1][xc][xp] = split_lo(v, hi);
   };
   f32x16 acc[2] = {f32x16{}, f32x16{}};
-  const int nstages = (int)((mrel_end + NS * kBfStage - 1) / (NS * kBfStage)) * NS;   // (extra stages add zeros)
-  load(std::integral_constant<int, 0>{}, 0);
-  // iteration st (set st mod NS): stage st+NS-1's loads into the set stage st-1 used; stage st's
-  // splits and MFMAs
-  auto iteration = [&](auto it_c, int st) __attribute__((always_inline)) {
-    constexpr int SET = decltype(it_c)::value;
-    using Ld = std::integral_constant<int, (SET + NS - 1) % NS>;
-    load(Ld{}, st + NS - 1);
-    __builtin_amdgcn_sched_barrier(0);
+  const int nstages = (int)((m1 - m0 + 2 * kBfStage - 1) / (2 * kBfStage)) * 2;   // even; the extra reads zeros
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(S0{}, 0);
+  load(S1{}, 1);
+  store_x(S0{}, 0);
+  __syncthreads();
+  // iteration st: split stage st's a (set st % 2) in registers, reuse the set for stage st+2's loads,
+  // stage st's MFMAs (x from LDS buffer st % 2), stage st+1's x into the other buffer
+  auto iteration = [&](auto set_c, int st) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_c)::value;
+    using Other = std::integral_constant<int, 1 - SET>;
+    const int buf = SET;
 #pragma unroll
     for (int j = 0; j < 8; ++j) bacc += (double)ra[SET][j];
-    h16x8 fh, fl, xh[2], xl[2];
+    h16x8 fh, fl;
     split2_f16(ra[SET], sa, fh, fl);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) split2_f16(rx[SET][t], sx, xh[t], xl[t]);
+    load(set_c, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      f32x16 v = mfma16(fl, xh[t], acc[t]);   // small products first
-      v = mfma16(fh, xl[t], v);
-      acc[t] = mfma16(fh, xh[t], v);
+      const h16x8 xh = *reinterpret_cast<const h16x8*>(&Xs[buf][0][32 * t + c][8 * h]);
+      const h16x8 xl = *reinterpret_cast<const h16x8*>(&Xs[buf][1][32 * t + c][8 * h]);
+      f32x16 v = mfma16(fl, xh, acc[t]);   // small products first
+      v = mfma16(fh, xl, v);
+      acc[t] = mfma16(fh, xh, v);
     }
+    store_x(Other{}, buf ^ 1);   // (after the last stage: zeros into the idle buffer)
+    __syncthreads();
   };
-  static_assert(kPairStages == 2, "the unrolled loop below");
-  for (int st = 0; st < nstages; st += NS) {
-    iteration(std::integral_constant<int, 0>{}, st);
-    iteration(std::integral_constant<int, 1>{}, st + 1);
+  for (int st = 0; st < nstages; st += 2) {
+    iteration(S0{}, st);
+    iteration(S1{}, st + 1);
   }
   // acc = sum (a 2^(14-Ea)) (x 2^(14-Ex)): unscaled here by two exact power-of-two factors (each
   // normal for any exponent the clamps allow)
@@ -2748,7 +2750,7 @@ block_head_sums_kernel(const float* __restrict__ grad, const float* __restrict__
 // The ray-sum buffers for any N >= kRaySumMinN (B = M / N <= M / kRaySumMinN rays): region A holds
 // S (B x 256, ray_sums_kernel) or the fused path's 8-sample sums of d pre_dir ((M / 8) x 128), region
 // B the fused path's S_hd ((M / 32) x 128), region C E (B x 32).
-constexpr int kRaySumMinN = 32;
+constexpr int kRaySumMinN = kEncDPerRayMinN;   // (enc_d per ray from there on, layout.h)
 static size_t ray_sum_a_floats(int64_t M) { return (size_t)(M / 8 + 1) * kDirHidden; }   // >= (M / 32 + 1) 256
 static size_t ray_sum_b_floats(int64_t M) { return (size_t)(M / 32 + 1) * kDirHidden; }
 static size_t ray_sum_floats(int64_t M) { return ray_sum_a_floats(M) + ray_sum_b_floats(M) + (size_t)(M / 32 + 1) * 32 + 64; }

@@ -73,7 +73,8 @@ int nerf_pack_weights_transposed_host(const float* const* params, float* packedT
 int nerf_ray_features_train(const float* packed, const float* dirs, int64_t R, const float* app,
                             int64_t app_rows, float* feat, float* enc_d, nerf_stream_t stream);
 /* nerf_mlp_forward (no scatter) that also writes save (NERF_TILE_ROWS(R*N), NERF_SAVE_ROW,
- * tile-major, padding rows zeroed) and, under the f16x3
+ * tile-major, padding rows zeroed; enc_d, constant along a ray, only in each ray's first row when
+ * N >= 32) and, under the f16x3
  * arithmetic, masks (R*N, NERF_MASK_ROW) (required there; ignored under f32, may be null). */
 int nerf_mlp_forward_train(const float* packed, const float* origins, const float* dirs,
                            const float* z_vals, int64_t R, int N, const float* ray_feat,
