@@ -52,11 +52,13 @@ FLOP_WGRAD = 2 * (64 * 256 + 6 * 257 * 256 + 320 * 256 + 257 + 284 * 128 + 33 * 
 # dir/sigma) on split-f16 with per-chunk power-of-two scales (three f16 products per fp32 product:
 # 2516.8/3 = 838.9 TFLOP/s; vendor f16 GEMM 1,323.5 / 3).
 # HBM: bytes the weight-gradient phase must read once per sample (fp32 rows, layout.h): gradient rows
-# d pre_0..7 (8 x 256), [d pre_dir | d sigma] (129), d hd (128), d rgb (3); saved rows enc_x (63),
-# h_0..h_7 (8 x 256), hd (128).  Against 8 TB/s this is the phase's binding roofline under f16x3
-# (0.60 ms per 262,144 samples, against 0.33 ms of MFMA work at 838.9 TFLOP/s).
+# d pre_0..7 (8 x 256), [d pre_dir | d sigma] (129), d rgb (3); saved rows enc_x (63), h_0..h_7
+# (8 x 256), hd (128).  (d hd's 128 columns were read per sample until round 5; under f16x3 the per-ray
+# sums now come from the dir/density launch and the block sums of d rgb, train.hip.)  Against 8 TB/s
+# this is the phase's binding roofline under f16x3 (0.58 ms per 262,144 samples, against 0.33 ms of
+# MFMA work at 838.9 TFLOP/s).
 HBM_PEAK_GBS = 8000.0
-WGRAD_ALG_BYTES = 4 * (8 * 256 + 129 + 128 + 3 + 63 + 8 * 256 + 128)   # 18,188
+WGRAD_ALG_BYTES = 4 * (8 * 256 + 129 + 3 + 63 + 8 * 256 + 128)   # 17,676
 WGRAD_ARITH, WGRAD_PRODUCTS, WGRAD_VENDOR = "block-scaled f16x3", 3, 1323.5 / 3
 
 
@@ -110,7 +112,7 @@ def pmc_traffic():
         k = json.load(open(PMC_SUMMARY))["kernels"]
         bw = next(v for n, v in k.items() if "mlp_backward16" in n)   # (the LDS-stream kernel since r02)
         wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items()
-                    if "wgrad" in n or "ray_sums" in n)   # the parameter-gradient phase (param_grads)
+                    if "wgrad" in n or "ray_sums" in n or "block_head_sums" in n or "app_grad" in n)   # param_grads
         return {"wgrad": wgrad / bw["dispatches"], "mlp_backward": bw["hbm_bytes_per_dispatch"]}
     except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
         return {}

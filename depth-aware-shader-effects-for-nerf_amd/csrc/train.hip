@@ -875,7 +875,7 @@ __global__ void __launch_bounds__(64 * kW16Waves, 1)
 mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __restrict__ packedT,
                             const uint32_t* __restrict__ masks, const float* __restrict__ sigma,
                             const float* __restrict__ rgb, const float* __restrict__ dsigma,
-                            const float* __restrict__ drgb, int64_t M, float* __restrict__ grad) {
+                            const float* __restrict__ drgb, int64_t M, float* __restrict__ grad, int store_dhd) {
   __shared__ __attribute__((aligned(16))) float lds[kBoLdsFloats];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5;
   const int64_t s0 = ((int64_t)blockIdx.x * kW16Waves + wave) * 32;
@@ -948,8 +948,9 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
           dhd[t][4 * q + e] = b[e];
           m_dir = fmaxf(m_dir, fabsf(b[e]));
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows, (int)ga.loff,
-                                               4 * (int)tile_col(kGradHd + 32 * t + 8 * q), 0);
+        if (store_dhd)   // (uniform; the training step's fused per-ray sums read none, param_grads)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows, (int)ga.loff,
+                                                 4 * (int)tile_col(kGradHd + 32 * t + 8 * q), 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), ga.rows, (int)ga.loff,
                                                4 * (int)tile_col(kGradDir + 32 * t + 8 * q), 0);
       }
@@ -1099,9 +1100,11 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
                                         (int)ga.loff + 4 * (int)(tile_col(kMetaGradF) + kMetaGradF % 8), 0, 0);
 }
 
+// store_dhd = false (nerf_train_backward on the fused path of param_grads): the mask-row kernel leaves
+// the d hd columns of the gradient rows unwritten (nothing reads them there).
 int launch_mlp_backward(const float* packed, const float* packedT, const float* save, const uint32_t* masks,
                         const float* sigma, const float* rgb, const float* dsigma, const float* drgb, int64_t M,
-                        float* grad, hipStream_t s) {
+                        float* grad, hipStream_t s, bool store_dhd = true) {
   if (M == 0) return NERF_OK;
   // tile-major gradient rows: the last block's rows past M are zeros (layout.h); its tail lanes store nothing
   if (M % 32 && hipMemsetAsync(grad + (M / 32) * 32 * kGradRow, 0, (size_t)32 * kGradRow * 4, s) != hipSuccess)
@@ -1109,7 +1112,7 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
   if (g_mlp_arith == NERF_ARITH_F16X3) {
     if (masks)
       hipLaunchKernelGGL(mlp_backward16_bound_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
-                         packedT, masks, sigma, rgb, dsigma, drgb, M, grad);
+                         packedT, masks, sigma, rgb, dsigma, drgb, M, grad, (int)store_dhd);
     else
       hipLaunchKernelGGL(mlp_backward16_kernel, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, packed,
                          packedT, save, sigma, rgb, dsigma, drgb, M, grad);
@@ -1913,7 +1916,10 @@ wgrad_h16h_kernel(const float* __restrict__ a, int64_t lda, const float* __restr
   const int h = lane >> 5, c = lane & 31;
   const uint32_t lda4 = (uint32_t)lda * 4u, ldx4 = (uint32_t)ldx * 4u;
   const int ac = 128 * half + (tid & 127), as0 = 8 * (tid >> 7);   // the thread's a column, its first sample
-  const uint32_t avo = ac < nrows ? 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0 : 0x80000000u;
+  // a columns past the kept rows' whole feature groups (meta.a_cols; the dir/density launch: 129 of 160
+  // -> 136) are not read: their rows are dropped, and an offset beyond the resource reads 0
+  const int acols = (meta.a_cols + 7) / 8 * 8 < nrows ? (meta.a_cols + 7) / 8 * 8 : nrows;
+  const uint32_t avo = ac < acols ? 4u * (uint32_t)(tile_col(ac) + ac % 8) + 32u * (uint32_t)as0 : 0x80000000u;
   uint32_t xvo[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -2751,6 +2757,9 @@ block_head_sums_kernel(const float* __restrict__ grad, const float* __restrict__
 // S (B x 256, ray_sums_kernel) or the fused path's 8-sample sums of d pre_dir ((M / 8) x 128), region
 // B the fused path's S_hd ((M / 32) x 128), region C E (B x 32).
 constexpr int kRaySumMinN = kEncDPerRayMinN;   // (enc_d per ray from there on, layout.h)
+// The fused per-ray sums (the split arithmetic's dir/density launch writes d pre_dir's 8-sample sums,
+// block_head_sums_kernel the rest): 32-sample blocks on one ray.  Then nothing reads d hd's columns.
+static bool fused_ray_sums(int N) { return g_mlp_arith == NERF_ARITH_F16X3 && N >= kRaySumMinN && N % 32 == 0; }
 static size_t ray_sum_a_floats(int64_t M) { return (size_t)(M / 8 + 1) * kDirHidden; }   // >= (M / 32 + 1) 256
 static size_t ray_sum_b_floats(int64_t M) { return (size_t)(M / 32 + 1) * kDirHidden; }
 static size_t ray_sum_floats(int64_t M) { return ray_sum_a_floats(M) + ray_sum_b_floats(M) + (size_t)(M / 32 + 1) * 32 + 64; }
@@ -3057,7 +3066,7 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     hm.a_cols = kDirHidden + 1;                            // d pre_dir, d sigma (rows 129.. are dropped)
     // fused: the split arithmetic's dir/density launch (wgrad_h16h_kernel) writes d pre_dir's 8-sample
     // sums, and blocks of 32 samples lie on one ray
-    const bool fused = g_mlp_arith == NERF_ARITH_F16X3 && N % 32 == 0;
+    const bool fused = fused_ray_sums(N);
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
                            M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm,
                            fused ? S : nullptr)))
@@ -3233,7 +3242,7 @@ int nerf_train_backward(const float* packed, const float* packedT, const float* 
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, R(T_SQE), B, loss);
   if ((rc = check_launch("loss_kernel"))) return rc;
   if ((rc = launch_mlp_backward(packed, packedT, R(T_SAVE), masks, R(T_SIG), R(T_RGB), R(T_DSIG), R(T_DRGB), M,
-                                R(T_GRAD), s)))
+                                R(T_GRAD), s, /*store_dhd=*/!fused_ray_sums(N))))
     return rc;
   const size_t wg_floats = (need - off[T_WG]) / 4;
   return param_grads(R(T_SAVE), R(T_GRAD), M, N, app, app_rows, packed, param_grads_out, dapp, R(T_WG), wg_floats, s);
