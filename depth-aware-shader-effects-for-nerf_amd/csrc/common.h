@@ -138,6 +138,9 @@ extern int g_mlp_arith;   // nerf_arith, set by nerf_set_mlp_arith
 int launch_mlp16(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s,
                  float* save = nullptr, const float* encd = nullptr, uint32_t* masks = nullptr);
+// the render MLP on 16 x 16 x 32 tiles (mlp16s.hip): launch_mlp16 without saves
+int launch_mlp16s(const float* packed, const float* o, const float* d, const float* z, int64_t R, int N,
+                  const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T, hipStream_t s);
 int launch_mlp(const float* packed, const float* o, const float* d, const float* z, int64_t R,
                int N, const float* feat, float* rgb, float* sigma, const int* out_slot, int out_T,
                hipStream_t s, float* save = nullptr, const float* encd = nullptr, uint32_t* masks = nullptr);

@@ -548,12 +548,9 @@ int launch_mlp16(const float* packed, const float* o, const float* d, const floa
   // tile-major save rows: the last block's rows past M are zeros (layout.h), its tail lanes store nothing
   if (save && M % 32 && hipMemsetAsync(save + (M / 32) * 32 * kSaveRow, 0, (size_t)32 * kSaveRow * 4, s) != hipSuccess)
     return set_error(NERF_ERR_HIP, "mlp16 training forward: hipMemsetAsync failed");
-  if (save)
-    hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, save, encd, masks);
-  else
-    hipLaunchKernelGGL(mlp16_kernel<false>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
-                       feat, rgb, sigma, out_slot, out_T, nullptr, nullptr, nullptr);
+  if (!save) return launch_mlp16s(packed, o, d, z, R, N, feat, rgb, sigma, out_slot, out_T, s);
+  hipLaunchKernelGGL(mlp16_kernel<true>, dim3((unsigned)blocks), dim3(64 * kW16Waves), 0, s, packed, o, d, z, M, N,
+                     feat, rgb, sigma, out_slot, out_T, save, encd, masks);
   return check_launch("mlp16_kernel");
 }
 

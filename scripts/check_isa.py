@@ -34,8 +34,8 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-DEFAULT_KERNELS = r"mlp16_kernel|mlp_backward16"
-DEFAULT_STREAMS = r"mlp16_kernel|mlp_backward16_bound"
+DEFAULT_KERNELS = r"mlp16_kernel|mlp16s_kernel|mlp_backward16"
+DEFAULT_STREAMS = r"mlp16_kernel|mlp16s_kernel|mlp_backward16_bound"
 IMPLICIT_M0 = re.compile(r"^(s_movrel|v_movrel|s_set_gpr_idx|ds_\w*addtid|ds_gws_|ds_append|ds_consume|"
                          r"ds_ordered_count|s_sendmsg|v_interp|s_ttracedata)")
 LDS_DMA = re.compile(r"^(global_load_lds_|buffer_load_\w+.*\blds\b|buffer_load_lds_)")
@@ -160,6 +160,7 @@ def check_function(insns):
 # certain are not counted (counting an op that the hardware does not would be the unsafe direction).
 STREAM_PIECES = (  # (kernel regex, this wave's pieces per published chunk / stage)
     (r"mlp16_kernel", 4),
+    (r"mlp16s_kernel", 4),
     (r"mlp_backward16_bound_kernel", 4),
 )
 VM_OP = re.compile(r"^(global_|buffer_(load|store|atomic)|scratch_)")

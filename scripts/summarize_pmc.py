@@ -13,7 +13,8 @@ the pass that collected GRBM_GUI_ACTIVE, and
     (1024 SIMDs x GRBM_GUI_ACTIVE / 8), per dispatch from the pass that collected them (its own
     duration), averaged over the dispatches; a dispatch whose derived clock exceeds the part's 2.4
     GHz maximum carries a corrupt counter and is dropped (listed under "notes").
-Top-level mlp_* fields describe the render MLP (mlp16_kernel<false>, else mlp_kernel), averaged over
+Top-level mlp_* fields describe the render MLP (mlp16s_kernel; mlp16_kernel<false> until round 5; else
+mlp_kernel), averaged over
 its dispatches of every grid size (bench.py's traffic per average launch)."""
 import collections
 import csv
@@ -82,7 +83,7 @@ def summarize(src):
             kk["l2_hit_rate"] = kk["TCC_HIT_sum"] / max(kk["TCC_HIT_sum"] + kk["TCC_MISS_sum"], 1.0)
         res["kernels"][key] = kk
     # the render MLP over all its grid sizes (dispatch-weighted)
-    for mlp in ("nerf::mlp16_kernel<false>", "nerf::mlp_kernel"):
+    for mlp in ("nerf::mlp16s_kernel", "nerf::mlp16_kernel<false>", "nerf::mlp_kernel"):
         keys = [k for k in res["kernels"] if k.split("|")[0] == mlp]
         if keys:
             break

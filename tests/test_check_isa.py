@@ -90,7 +90,7 @@ def disasm():
 
 def test_shipped_library_is_clean(disasm):
     report, checked = check_isa.check(disasm)
-    assert any("mlp16_kernel<false>" in n for n in checked) and any("mlp16_kernel<true>" in n for n in checked)
+    assert any("mlp16s_kernel" in n for n in checked) and any("mlp16_kernel<true>" in n for n in checked)
     assert any("mlp_backward16_bound_kernel" in n for n in checked)
     assert report == {}, report
 
@@ -111,7 +111,7 @@ def _insert(text, kernel, line, after=5):
     return "\n".join(out)
 
 
-@pytest.mark.parametrize("kernel", ["mlp16_kernel<false>", "mlp_backward16_bound_kernel"])
+@pytest.mark.parametrize("kernel", ["mlp16s_kernel", "mlp_backward16_bound_kernel"])
 @pytest.mark.parametrize("line", ["s_movrel_b32 s0, s1", "ds_read_addtid_b32 v0", "s_mov_b32 s3, m0",
                                   "s_mov_b32 m0, 0x100", "v_readfirstlane_b32 s2, v1 ; s_add_u32 s2, s2, m0"])
 def test_inserted_m0_reader_is_caught(disasm, kernel, line):
@@ -133,7 +133,7 @@ def test_unconsumed_m0_write_is_caught(disasm):
 # ---- counted vmcnt waits of the LDS-DMA streams (check_isa.check_vmcnt) ---------------------------
 def test_stream_kernels_are_checked(disasm):
     report, checked = check_isa.check(disasm)
-    for k in ("mlp16_kernel<true>", "mlp16_kernel<false>", "mlp_backward16_bound_kernel"):
+    for k in ("mlp16_kernel<true>", "mlp16s_kernel", "mlp_backward16_bound_kernel"):
         assert any(k in n for n in checked), k
     assert report == {}, report
 
