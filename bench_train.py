@@ -112,7 +112,7 @@ def pmc_traffic():
         k = json.load(open(PMC_SUMMARY))["kernels"]
         bw = next(v for n, v in k.items() if "mlp_backward16" in n)   # (the LDS-stream kernel since r02)
         wgrad = sum(v["hbm_bytes_per_dispatch"] * v["dispatches"] for n, v in k.items()
-                    if "wgrad" in n or "ray_sums" in n or "block_head_sums" in n or "app_grad" in n)   # param_grads
+                    if "wgrad" in n or "ray_sums" in n or "app_grad" in n)   # param_grads
         return {"wgrad": wgrad / bw["dispatches"], "mlp_backward": bw["hbm_bytes_per_dispatch"]}
     except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
         return {}

@@ -77,6 +77,25 @@ __device__ __forceinline__ uint32_t split_lo_pair(uint32_t hi2, float x0, float 
 constexpr int kRowStoreAux = 2;
 constexpr int kRowLoadAux = 0;
 
+// A 16-byte row store with its whole offset in the lane's VGPR `voff` (+ the instruction's offset
+// field) and soffset the literal 0.  For a store of more than 8 bytes whose soffset is a register, the
+// compiler's hazard model pads no wait states before an instruction that overwrites the store's data
+// VGPRs, and a uniform or large constant soffset is always a register.  Measured on gfx950 (round 6,
+// scripts/diag_train_det.py): in the training forward a `v_accvgpr_read` into the first data VGPR
+// right behind a `buffer_store_dwordx4 ..., s60` that followed an LDS-DMA issue reached the register
+// before the store read it; that activation (one float of the four, both lane halves) came out
+// different from run to run.  With soffset 0 the compiler pads those wait states (and
+// scripts/check_isa.py rejects a data VGPR written within two of them in the stream kernels).
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+// PAD: two wait states right behind the store in an asm statement, which no memory instruction is
+// scheduled across (a load whose destination is one of the data VGPRs; the compiler pads only VALU).
+template <int AUX, bool PAD = false, typename V>
+__device__ __forceinline__ void store16_rows(V v, __amdgpu_buffer_rsrc_t rows, uint32_t voff) {
+  static_assert(sizeof(V) == 16, "16-byte stores");
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4s, v), rows, (int)voff, 0, AUX);
+  if constexpr (PAD) asm volatile("s_nop 1");
+}
+
 __device__ __forceinline__ float expf_rn(float x) { return (float)exp((double)x); }
 
 // Max over the wave of a non-negative v, uniform result: DPP within each 16-lane row (quad swaps,

@@ -101,12 +101,11 @@ __device__ __forceinline__ void mask_or(const SaveAt& sv, int T, uint32_t bits) 
   __hip_atomic_fetch_or(sv.mrow + sv.mlay + T / 2, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 // 16 bytes at byte offset voff + 4 * (hoff + c) of the wave's rows: a buffer store, so the lane's
-// address stays one VGPR (the uniform slice goes in soffset, the constant in the offset field).
+// address stays one VGPR (store16_rows, common.h: the whole offset in the VGPR, soffset 0).
 // (tile-major rows, layout.h: feature group c / 8 of the slice at hoff; c and hoff multiples of 8, so
 // one store instruction writes the wave's 32 samples x 8 features, 1 KiB, contiguously)
 __device__ __forceinline__ void save_store(const SaveAt& sv, int c, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), sv.rows, (int)sv.loff + 4 * (int)tile_col(c),
-                                         4 * (int)tile_col(sv.hoff), kRowStoreAux);
+  store16_rows<kRowStoreAux>(v, sv.rows, sv.loff + 4u * (uint32_t)tile_col(sv.hoff) + 4u * (uint32_t)tile_col(c));
 }
 template <int T0, int QG, bool SIGMA>
 __device__ __forceinline__ void load4(const float* bias, const float* ws, int h, QuarterVec& qv) {
@@ -360,8 +359,12 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
   };
   using NoSigma = std::false_type;
   using Sigma = std::true_type;
-#pragma unroll 1
-  for (int L = 1; L < 8; ++L) {
+  // One trunk layer (SKIP: layer 4 reads [h3, enc_x], 10 chunk-steps per group; SG: layer 7 starts
+  // the density head).  Layers 1-3 and 5-6 run as loops of the plain body, layers 4 and 7 on their
+  // own: one body with the variants behind runtime branches spilled 16 VGPRs in the training forward
+  // (the register allocator serves every variant's live ranges at the loop's back edge).
+  auto layer = [&](int L, auto skip_tag, auto sg_tag) __attribute__((always_inline)) {
+    constexpr bool SKIP = decltype(skip_tag)::value;
     inv_cur = cst[kS16InvW + L] / s_cur;
     const float* bias_l = bias + L * kHidden;
     const int c0 = s16_chunk0(1) + (L - 1) * 16 + (L > kSkipLayer ? 4 : 0);
@@ -372,7 +375,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
       sv_cur.mlay = (kMaskLayerBytes / 4) * L;
     }
     // group A (k-steps 0..15, + PE 16..19 at layer 4)
-    if (L == kSkipLayer) {
+    if constexpr (SKIP) {
       // layer 4 reads [h3, enc_x]: its PE operands are split at s_cur at hs 15..18 (PE operand q is
       // read at hs 16 + q)
       run_group<0, 10, 0, 3, kSideSkipPrev, SAVE>(stream, c0, lds, lds_dma, voff, a0, a1, acc, lane, op4,
@@ -393,26 +396,29 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
       const float rec = block_exp_record(wave_max_nn(m));
       bexp = (lane & 31) == L - 1 ? rec : bexp;
     }
-    float bound = cst[kS16R + L] * (L == kSkipLayer ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
+    float bound = cst[kS16R + L] * (SKIP ? fmaxf(m, m_pe) : m) + cst[kS16B + L];
     if (L + 1 == kSkipLayer) bound = fmaxf(bound, m_pe);    // layer 4 splits the PE at the same scale
     s_nxt = pow2_scale(bound);
     m = 0.0f;
     // group B (layer 7 also starts the density head)
-    if (L == kSkipLayer) {
+    if constexpr (SKIP) {
       run_group<1, 10, 2, 3, kSideCur, SAVE>(stream, c0 + 10, lds, lds_dma, voff, a0, a1, acc, lane, op4,
                              [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
-    } else if (L == 7) {
-      run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, Sigma{}); });
     } else {
       run_group<1, 8, 0, 3, kSideCur, SAVE>(stream, c0 + 8, lds, lds_dma, voff, a0, a1, acc, lane, act_operand,
-                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, NoSigma{}); });
+                            [&](auto i, auto kk, auto ph) __attribute__((always_inline)) { side_cur(i, kk, ph, bias_l, sg_tag); });
     }
     inv_prev = inv_cur;
     bias_prev = bias_l;
     s_cur = s_nxt;
     STAMP16(2 + L);
-  }
+  };
+#pragma unroll 1
+  for (int L = 1; L < kSkipLayer; ++L) layer(L, NoSigma{}, NoSigma{});
+  layer(kSkipLayer, std::true_type{}, NoSigma{});
+#pragma unroll 1
+  for (int L = kSkipLayer + 1; L < 7; ++L) layer(L, NoSigma{}, NoSigma{});
+  layer(7, NoSigma{}, Sigma{});
 
   // ---- colour layer: h7 -> 128 (one group, 8 chunk-steps); its side converts y_7 tiles 4-7 into
   // operands 8..15 and finishes the density head ----
@@ -522,8 +528,7 @@ mlp16_kernel(const float* __restrict__ packed, const float* __restrict__ orig, c
         for (int q = 0; q < 4; ++q)
         {   // features kSaveEncD + 16h + 4q .. +3 of the sample (tile-major: group, then 4 of its 8)
           const int F = kSaveEncD + 16 * h + 4 * q;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ed[q]), wrows,
-                                                 (int)loff - 16 * h + 4 * (int)(tile_col(F) + F % 8), 0, 0);
+          store16_rows<0>(ed[q], wrows, loff - 16u * h + 4u * (uint32_t)(tile_col(F) + F % 8));
         }
       }
     }

@@ -477,7 +477,7 @@ __device__ __forceinline__ T* tile_row(T* base, int64_t s, int R) {
 
 // 16 bytes at feature off (+ 4 h) of this lane's gradient row (off a multiple of 8)
 __device__ __forceinline__ void grad_store4(const GradRows& g, int off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), g.res, (int)g.loff, 4 * (int)tile_col(off), 0);
+  store16_rows<0>(v, g.res, g.loff + 4u * (uint32_t)tile_col(off));
 }
 
 // d pre-activation = d activation * [activation > 0] (ReLU backward; the saved activation is
@@ -844,9 +844,8 @@ __device__ __forceinline__ void bw_convert4(const f32x16 (&acc)[8], float inv, f
     m = fmaxf(m, fabsf(d));          // (layer 0, SPLIT = false: its block exponent record)
     if constexpr (SPLIT) xs[e] = d * s;
   }
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dv), g.rows,
-                                         (int)g.loff + 4 * (int)tile_col(32 * T + 8 * q), 4 * (int)tile_col(g.slice),
-                                         kRowStoreAux);
+  store16_rows<kRowStoreAux, true>(dv, g.rows,
+                                   g.loff + 4u * (uint32_t)tile_col(g.slice) + 4u * (uint32_t)tile_col(32 * T + 8 * q));
   if constexpr (SPLIT) {   // hi pairs by v_cvt_pk_f16_f32, lo pairs by split_lo_pair
     Operand& op = in[OP0 + QG / 2];
     typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
@@ -949,10 +948,8 @@ mlp_backward16_bound_kernel(const float* __restrict__ packed, const float* __res
           m_dir = fmaxf(m_dir, fabsf(b[e]));
         }
         if (store_dhd)   // (uniform; the training step's fused per-ray sums read none, param_grads)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), ga.rows, (int)ga.loff,
-                                                 4 * (int)tile_col(kGradHd + 32 * t + 8 * q), 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), ga.rows, (int)ga.loff,
-                                               4 * (int)tile_col(kGradDir + 32 * t + 8 * q), 0);
+          store16_rows<0>(a, ga.rows, ga.loff + 4u * (uint32_t)tile_col(kGradHd + 32 * t + 8 * q));
+        store16_rows<0>(b, ga.rows, ga.loff + 4u * (uint32_t)tile_col(kGradDir + 32 * t + 8 * q));
       }
   }
   m_dir = sample_max(m_dir);
@@ -1129,7 +1126,7 @@ int launch_mlp_backward(const float* packed, const float* packedT, const float* 
 // (x_div = 1: a per-sample input; = N: a per-ray input; 0: one broadcast row).  Each chunk's
 // partial occupies wgrad_stride(N, K) floats (N*KP rounded up to 4, for 16-byte reduce loads, + 4).
 constexpr int kWChunk = 2048;   // samples per chunk
-// Chunk length of a (N, K) weight gradient on the bf16x6 path: short enough that a 2^18-sample
+// Chunk length of a (N, K) weight gradient outside the split-f16 GEMMs: short enough that a 2^18-sample
 // step puts a block in every resident slot.  The 256x64-tile launches (K <= 64, N > 64: layer 0
 // and the appearance projection) hold one block per CU and have one tile: 1024-sample chunks give
 // 256 blocks instead of 128.  The 128x128-tile launches hold two blocks per CU; those with fewer
@@ -1140,8 +1137,11 @@ static inline bool wgrad_whole_tile(int N, int K) { return (N == 256 || N == 160
 // launches are bound by HBM, not MFMA, and halving the chunk partials (~0.5 GB per step written and
 // read back) paid +1.7 % on the training step against 1,024-sample chunks (same-box A/B,
 // profiles/r05/ab_head3_pe_clen2k.log; under bf16x6 the 2,048-sample chunks had been 3.5 % slower).
+// (Round 6, same box: 4,096-sample whole-tile chunks -11 % on the step, 64 chunks leave CUs idle; the
+// layer-0 / skip-PE pair on 2,048-sample chunks instead of 1,024 +1.1 %, its partials halved:
+// profiles/r06/ab_train_chunks.log.)
 constexpr int kWholeClen = kWChunk, kWholeMinChunks = 128;       // whole-tile chunk length, minimum chunk count
-constexpr int kPairClen = kWChunk / 2, kPairMinChunks = 256;      // the layer-0 / skip-PE pair's
+constexpr int kPairClen = kWChunk, kPairMinChunks = 128;          // the layer-0 / skip-PE pair's
 static inline int wgrad_chunk_len_big(int N, int K) {
   if (wgrad_whole_tile(N, K)) return kWholeClen;   // one block per chunk, 256 per step
   if (K <= 64 && N == 2 * kHidden) return kPairClen;   // (the layer-0 / skip-PE pair)
@@ -1350,7 +1350,9 @@ wgrad_lds_kernel(const float* __restrict__ a, int64_t lda, int N, const float* _
   }
 }
 
-// The weight-gradient kernel of the split MLP arithmetic ("bf16x6", nerf_arith F16X3): the same
+// The bf16x6 weight-gradient kernel of the split MLP arithmetic (nerf_arith F16X3; the GEMMs the
+// split-f16 kernels below do not take: in training the per-ray GEMMs over gradient sums, otherwise
+// nerf_wgrad's other shapes): the same
 // partial sums as wgrad_lds_kernel, on v_mfma_f32_32x32x16_bf16.  Every operand value is split into
 // three bf16 parts, x = b0 + b1 + b2 + O(2^-27 x) (each part the RNE bf16 of the f32 remainder, the
 // remainders exact), and a k-step accumulates the six products of order >= 2^-16,
@@ -2188,7 +2190,7 @@ wgrad_bf_k64_kernel(const float* __restrict__ a, int64_t lda, const float* __res
 // Layer 0's weight gradient (d pre_0 over enc_x) and the skip layer's PE columns (d pre_4 over enc_x)
 // of the split arithmetic as one 512 x 63 GEMM on split-f16 MFMA (wgrad_bf_k64_kernel<true, 16>'s
 // shape with wgrad_h16h_kernel's arithmetic: three f16 products per fp32 product instead of bf16x6's
-// six, two f16 parts to split instead of three bf16 parts).  16 waves per 1,024-sample chunk: wave w
+// six, two f16 parts to split instead of three bf16 parts).  16 waves per chunk (kPairClen): wave w
 // owns output rows 32w .. 32w+31 (waves 0-7 of d pre_0, 8-15 of d pre_4; one MFMA row tile, two
 // column tiles), loads its a columns straight in A-fragment order and splits them in registers; x =
 // enc_x (63 columns + the pad slot, which is never read) is split once per workgroup into LDS, one
@@ -2361,10 +2363,27 @@ wgrad_pair16_kernel(const float* __restrict__ grad, const float* __restrict__ sa
 // 3 x 4 products in double; at the chunk's end the 32 lanes of each parity are summed (shuffles,
 // double) into the chunk's partial (N = 3, K = 128 layout of wgrad_reduce_kernel; the bias column
 // from wave 0).  Reads hd once at full lines: ~134 MB per 262K-sample step.
+// SUMS (rays of N % 32 == 0 samples under the split arithmetic, the fused per-ray sums): the launch
+// also writes what the appearance projection's and dir_linear's per-ray GEMMs need from the head,
+// since it holds every block's d rgb_pre anyway (models.py:154-160: d hd = W_rgb^T d rgb_pre is linear
+// in the sample, so a block's sum of d hd needs only its 3 column sums): per 32-sample block b (all on
+// one ray) S_hd[b] = W_rgb^T (the block's d rgb_pre sums, in double, rounded once), and for a ray's
+// first block E[ray] = the ray's PE_4(d) (its first sample's save row).  Wave (b - b0) % 4 takes
+// block b.  (Until round 6 a separate block_head_sums_kernel read the d rgb_pre rows again.)
 constexpr int kHeadChunkBlocks = 16;   // (512 chunks per 262K-sample step: two workgroups per CU)
+template <bool SUMS = false>
 __global__ void __launch_bounds__(256)
-wgrad_head3_kernel(const float* __restrict__ a, const float* __restrict__ x, int64_t M, float* __restrict__ partial) {
+wgrad_head3_kernel(const float* __restrict__ a, const float* __restrict__ x, int64_t M, float* __restrict__ partial,
+                   const float* __restrict__ save = nullptr, const float* __restrict__ packed = nullptr, int N = 0,
+                   float* __restrict__ S_hd = nullptr, float* __restrict__ E = nullptr) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float wr[3][2];   // SUMS: rgb_linear.weight columns lane, lane + 64
+  if constexpr (SUMS) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) wr[c][q] = packed[kOffRgbW + c * kDirHidden + 64 * q + lane];
+  }
   const int64_t nblk = (M + 31) / 32;
   const int64_t b0 = (int64_t)blockIdx.x * kHeadChunkBlocks;
   const int64_t b1 = b0 + kHeadChunkBlocks < nblk ? b0 + kHeadChunkBlocks : nblk;
@@ -2388,6 +2407,22 @@ wgrad_head3_kernel(const float* __restrict__ a, const float* __restrict__ x, int
 #pragma unroll
     for (int g = 0; g < 4; ++g) v[g] = v_n[g];
     if (b + 1 < b1) load(b + 1, dv_n, v_n);
+    if constexpr (SUMS) {
+      if ((int)((b - b0) & 3) == w) {   // (wave-uniform)
+        double ds[3];   // lane (j, par) holds sample j's d rgb_pre: xor 2 .. 32 sums one parity's 32 lanes
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          ds[c] = (double)dv[c];
+#pragma unroll
+          for (int m = 2; m < 64; m <<= 1) ds[c] += __shfl_xor(ds[c], m);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          S_hd[b * kDirHidden + 64 * q + lane] =
+              (float)(ds[0] * (double)wr[0][q] + ds[1] * (double)wr[1][q] + ds[2] * (double)wr[2][q]);
+        if ((b * 32) % N == 0 && lane < 32) E[(b * 32 / N) * 32 + lane] = save[tile_off(b * 32, kSaveEncD + lane, kSaveRow)];
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const double d = (double)dv[c];
@@ -2568,12 +2603,19 @@ static int launch_wgrad_lds(const float* a, int64_t lda, int N, const float* x, 
   return check_launch("wgrad_lds_kernel");
 }
 
+// sums (nullable): S_hd and E of the fused per-ray sums (rays of N % 32 == 0 samples), save / packed
+// the rows and weights they come from
+struct HeadSums { const float* save; const float* packed; int N; float* S_hd; float* E; };
 static int launch_wgrad_head3(const float* a, const float* x, int64_t M, float* out_w, float* out_b, float* ws,
-                              size_t ws_floats, hipStream_t s) {
+                              size_t ws_floats, hipStream_t s, const HeadSums* sums = nullptr) {
   if (M == 0) return NERF_OK;
   const int chunks = (int)(((M + 31) / 32 + kHeadChunkBlocks - 1) / kHeadChunkBlocks);
   if ((size_t)chunks * wgrad_stride(3, kDirHidden) > ws_floats) return set_error(NERF_ERR_WORKSPACE, "wgrad_head3: workspace");
-  hipLaunchKernelGGL(wgrad_head3_kernel, dim3((unsigned)chunks), dim3(256), 0, s, a, x, M, ws);
+  if (sums)
+    hipLaunchKernelGGL(wgrad_head3_kernel<true>, dim3((unsigned)chunks), dim3(256), 0, s, a, x, M, ws, sums->save,
+                       sums->packed, sums->N, sums->S_hd, sums->E);
+  else
+    hipLaunchKernelGGL(wgrad_head3_kernel<false>, dim3((unsigned)chunks), dim3(256), 0, s, a, x, M, ws);
   if (int rc = check_launch("wgrad_head3_kernel")) return rc;
   const int64_t cols4 = wgrad_stride(3, kDirHidden) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((cols4 + 63) / 64)), dim3(64 * kRedParts), 0, s, ws, chunks, 3,
@@ -2728,37 +2770,13 @@ ray_sums_kernel(const float* __restrict__ grad, const float* __restrict__ save, 
   if (t < 32) E[r * 32 + t] = save[tile_off(m0, kSaveEncD + t, kSaveRow)];
 }
 
-// Rays of N % 32 == 0 samples under the split arithmetic (the fused per-ray sums; the dir/density
-// launch writes d pre_dir's 8-sample sums, wgrad_h16h_kernel SUMS): per 32-sample block b (all on one
-// ray), S_hd[b] = the block's sum of d hd = W_rgb^T (the sum of its 32 d rgb_pre rows) (models.py:
-// 154-160: d hd = W_rgb^T d rgb_pre is linear in the sample, so the block sum needs the 3 column
-// sums; in double, rounded once), and for a ray's first block E[ray] = the ray's PE_4(d) (its first
-// sample's save row).  Reads 1 KiB of gradient rows per block instead of ray_sums_kernel's 256
-// columns per sample.
-__global__ void __launch_bounds__(128)
-block_head_sums_kernel(const float* __restrict__ grad, const float* __restrict__ save, const float* __restrict__ packed,
-                       int N, float* __restrict__ S_hd, float* __restrict__ E) {
-  __shared__ double dsum[3];
-  const int64_t b = blockIdx.x;
-  const int t = threadIdx.x;
-  if (t < 3) {   // the block's 32 d rgb_pre of column t, in sample order
-    double acc = 0.0;
-    for (int j = 0; j < 32; ++j) acc += (double)grad[tile_off(b * 32 + j, kGradRgb + t, kGradRow)];
-    dsum[t] = acc;
-  }
-  __syncthreads();
-  const float* W = packed + kOffRgbW;   // rgb_linear.weight (3 x 128)
-  S_hd[b * kDirHidden + t] =
-      (float)(dsum[0] * (double)W[t] + dsum[1] * (double)W[kDirHidden + t] + dsum[2] * (double)W[2 * kDirHidden + t]);
-  if ((b * 32) % N == 0 && t < 32) E[(b * 32 / N) * 32 + t] = save[tile_off(b * 32, kSaveEncD + t, kSaveRow)];
-}
-
 // The ray-sum buffers for any N >= kRaySumMinN (B = M / N <= M / kRaySumMinN rays): region A holds
 // S (B x 256, ray_sums_kernel) or the fused path's 8-sample sums of d pre_dir ((M / 8) x 128), region
 // B the fused path's S_hd ((M / 32) x 128), region C E (B x 32).
 constexpr int kRaySumMinN = kEncDPerRayMinN;   // (enc_d per ray from there on, layout.h)
 // The fused per-ray sums (the split arithmetic's dir/density launch writes d pre_dir's 8-sample sums,
-// block_head_sums_kernel the rest): 32-sample blocks on one ray.  Then nothing reads d hd's columns.
+// the rgb head's launch, wgrad_head3_kernel<true>, the rest): 32-sample blocks on one ray.  Then
+// nothing reads d hd's columns.
 static bool fused_ray_sums(int N) { return g_mlp_arith == NERF_ARITH_F16X3 && N >= kRaySumMinN && N % 32 == 0; }
 static size_t ray_sum_a_floats(int64_t M) { return (size_t)(M / 8 + 1) * kDirHidden; }   // >= (M / 32 + 1) 256
 static size_t ray_sum_b_floats(int64_t M) { return (size_t)(M / 32 + 1) * kDirHidden; }
@@ -3029,8 +3047,12 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
   // pair kernel; under f32 two K = 63 jobs on the f32 GEMM like every other weight gradient
   const bool pe_pair = g_mlp_arith == NERF_ARITH_F16X3;
   if (pe_pair && (rc = launch_wgrad_pe_pair(save, grad, M, g[0], g[1], g[8], wb, wfl, sb))) return rc;
+  // fused per-ray sums (the split arithmetic's dir/density launch writes d pre_dir's 8-sample sums,
+  // the rgb head's launch d hd's block sums; blocks of 32 samples lie on one ray): below, on stream B
+  const bool fused = rays && fused_ray_sums(N);
   for (const Job& j : jobs) {
     if (pe_pair && j.K == kPosEnc) continue;            // (in the pair above)
+    if (fused && j.a == kGradRgb) continue;             // (with the per-ray sums below)
     if (wgrad_workspace_floats(M, j.n, j.K) > wfl) return set_error(NERF_ERR_WORKSPACE, "param_grads: workspace");
     if (j.a == kGradRgb) {   // the rgb head: the streaming kernel (3 rows)
       if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[j.p], g[j.p + 1],
@@ -3052,8 +3074,8 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     // gradient (+ its bias column), row 128 the density head's, rows 129.. are dropped (h7 is read once).
     // dir_linear's PE_4(d) columns and the appearance projection take per-ray inputs: GEMMs over
     // per-ray (or per-block) gradient sums, which replace two M-row GEMMs: under the split arithmetic
-    // with N % 32 == 0 the dir/density launch itself writes d pre_dir's 8-sample sums and
-    // block_head_sums_kernel d hd's block sums from d rgb_pre; otherwise ray_sums_kernel reads the
+    // with N % 32 == 0 the dir/density launch itself writes d pre_dir's 8-sample sums and the rgb
+    // head's launch d hd's block sums from d rgb_pre; otherwise ray_sums_kernel reads the
     // 256 gradient columns of every sample.
     const int64_t B = M / N;
     float* S = rays;                                       // B x 256 (fused: S8, (M / 8) x 128)
@@ -3064,17 +3086,15 @@ static int param_grads_jobs(const float* save, const float* grad, int64_t M, int
     const WgradSplit heads{kDirHidden, g[P_SIGMA_W], kHidden, kHidden, g[P_SIGMA_B], kDirHidden + 1};
     H16Meta hm = block_exps(save, grad, 7, 7);
     hm.a_cols = kDirHidden + 1;                            // d pre_dir, d sigma (rows 129.. are dropped)
-    // fused: the split arithmetic's dir/density launch (wgrad_h16h_kernel) writes d pre_dir's 8-sample
-    // sums, and blocks of 32 samples lie on one ray
-    const bool fused = fused_ray_sums(N);
     if ((rc = launch_wgrad(grad + tile_col(kGradDir), kGradRow, kDirRows, save + tile_col(save_h(7)), kSaveRow, kHidden, 1,
                            M, g[P_DIR_W], kHidden + kDirEnc, g[P_DIR_B], 0, wb, sb, &heads, true, true, &hm,
                            fused ? S : nullptr)))
       return rc;
     if (fused) {
-      hipLaunchKernelGGL(block_head_sums_kernel, dim3((unsigned)(M / 32)), dim3(kDirHidden), 0, sb, grad, save, packed, N,
-                         S_hd, E);
-      if ((rc = check_launch("block_head_sums_kernel"))) return rc;
+      const HeadSums hs{save, packed, N, S_hd, E};   // (rgb_linear's weight gradient + S_hd, E)
+      if ((rc = launch_wgrad_head3(grad + tile_col(kGradRgb), save + tile_col(kSaveHd), M, g[P_RGB_W], g[P_RGB_B], wb, wfl,
+                                   sb, &hs)))
+        return rc;
       // dir_linear's PE_4(d) columns over the M / 8 rows of 8-sample sums (row m: samples 8m .. 8m+7,
       // ray 8m / N)
       if ((rc = launch_wgrad(S, kDirHidden, kDirHidden, E, 32, kDirEnc, N / 8, M / 8, g[P_DIR_W] + kHidden,

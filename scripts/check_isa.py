@@ -16,7 +16,8 @@ translation unit) and checks, in every kernel whose name matches --kernels:
   * the stream kernels (--streams) hold at least one DMA piece (the pattern is still what the
     stream emits).
 
-and, in the stream kernels (STREAM_PIECES), that every counted `s_waitcnt vmcnt(N)` publishing an
+that no instruction overwrites the data registers of a 12- or 16-byte store within 2 wait states of
+it (check_store_data), and, in the stream kernels (STREAM_PIECES), that every counted `s_waitcnt vmcnt(N)` publishing an
 LDS-DMA ring slot leaves in flight only pieces younger than the published chunk, on every path of the
 kernel's control-flow graph (check_vmcnt, below).
 
@@ -317,6 +318,49 @@ def check_vmcnt(insns, pieces_per_group, margins=None):
     return sorted(set(bad))
 
 
+# ---- store-data wait states ----------------------------------------------------------------------
+# A buffer/global store of more than 8 bytes reads its data VGPRs after it issues; an instruction that
+# writes one of them too soon can change what is stored.  The compiler models this only for stores
+# whose soffset is not a register (csrc/common.h store16_rows), and round 6 measured the unpadded case
+# corrupting saved activations in the training forward.  Checked: no instruction within 2 wait states
+# after such a store (s_nop N counts N + 1) writes one of its data registers.
+WIDE_STORE = re.compile(r"^(buffer_store_dwordx[34]|global_store_dwordx[34]|buffer_store_b(96|128)|"
+                        r"global_store_b(96|128))\b")
+REG_WRITER = re.compile(r"^(v_|ds_read|ds_load|buffer_load|global_load|scratch_load)")
+STORE_DATA_STATES = 2
+
+
+def _regs(op):
+    m = re.match(r"^([va])\[(\d+):(\d+)\]$", op)
+    if m:
+        return {f"{m.group(1)}{i}" for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    return {op} if re.match(r"^[va]\d+$", op) else set()
+
+
+def check_store_data(insns):
+    """Violations of the store-data wait states in one kernel's instruction list."""
+    bad = []
+    for i, ins in enumerate(insns):
+        op = ins.split()[0]
+        if not WIDE_STORE.match(op):
+            continue
+        ops = [o.strip() for o in ins[len(op):].split(",")]
+        data = _regs(ops[1] if op.startswith("global_") else ops[0])
+        states = 0
+        for nxt in insns[i + 1:]:
+            if states >= STORE_DATA_STATES:
+                break
+            nop = nxt.split()[0]
+            if nop == "s_nop":
+                states += int(nxt.split()[1], 0) + 1
+                continue
+            if REG_WRITER.match(nop) and "_lds" not in nop and _regs(nxt[len(nop):].split(",")[0].strip()) & data:
+                bad.append(f"{i}: {ins} -> {nxt} after {states} wait state(s)")
+                break
+            states += 1
+    return bad
+
+
 def check(text, kernels=DEFAULT_KERNELS, streams=DEFAULT_STREAMS):
     """{kernel: violations} over the kernels matching `kernels` (regex), and the checked names."""
     report, checked = {}, []
@@ -326,6 +370,7 @@ def check(text, kernels=DEFAULT_KERNELS, streams=DEFAULT_STREAMS):
             continue
         checked.append(name)
         bad, pieces = check_function(insns)
+        bad += check_store_data(insns)
         if pieces == 0 and re.search(streams, name):
             bad.append("no LDS-DMA piece found (the stream pattern changed: update this check)")
         for pat, per in STREAM_PIECES:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box validation: each step under its own time limit; stops at the first crash/abort/timeout
 # (status >= 124), continues past ordinary test failures.  Usage: scripts/gpu_check.sh step...
-#   steps: variants | pytest | pytest_all | parity | pytest_train | bench | bench_f32 | bench_train | smoke
+#   steps: pytest | pytest_all | parity | pytest_train | bench | bench_f32 | bench_train | smoke
 mkdir -p gpurun_out
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2

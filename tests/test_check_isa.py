@@ -13,7 +13,12 @@ or the exit drain removed (fails), and on committed disassemblies of three build
 (tests/golden/isa, scripts/make_isa_fixtures.py): the default, round 3's store-slack count (passes:
 within the window) and NERF16_WAIT_EXTRA=1 (fails at the group-boundary publishes).  On the GPU the
 passing builds train bit-identically to each other and the failing ones differ from run to run
-(profiles/r04/vmcnt_ab_overcount.log, scripts/vmcnt_ab.py): the check's boundary is the hardware's."""
+(profiles/r04/vmcnt_ab_overcount.log, scripts/vmcnt_ab.py): the check's boundary is the hardware's.
+
+Store data: no instruction may write a data register of a 12- or 16-byte store within 2 wait states of
+it (round 6: an unpadded VALU write behind a store with a register soffset changed saved activations
+from run to run; csrc/common.h store16_rows).  Shown on hand-written sequences, including the
+measured one, and on the shipped training forward with such a write inserted."""
 import gzip
 import os
 import re
@@ -179,3 +184,40 @@ def test_flat_op_in_flight_window_is_caught(disasm):
             break
     report, _ = check_isa.check("\n".join(lines))
     assert any("mlp16_kernel<true>" in n and any("flat op" in b for b in v) for n, v in report.items()), report
+
+
+# ---- store-data wait states (check_isa.check_store_data) -----------------------------------------
+@pytest.mark.parametrize("insns,n_bad", [
+    # the round-6 failure (training forward, scripts/diag_train_det.py): the first data VGPR of a
+    # 16-byte store with a register soffset overwritten by the next instruction
+    (["buffer_store_dwordx4 v[6:9], v20, s[24:27], s60 offen nt", "v_accvgpr_read_b32 v6, a84"], 1),
+    (["buffer_store_dwordx4 v[6:9], v20, s[24:27], 0 offen nt", "s_nop 1", "v_accvgpr_read_b32 v6, a84"], 0),
+    (["buffer_store_dwordx4 v[6:9], v20, s[24:27], 0 offen nt", "s_nop 0", "v_fma_f32 v9, v1, v2, v3"], 1),
+    (["buffer_store_dwordx4 v[6:9], v20, s[24:27], 0 offen nt", "v_mfma_f32_32x32x16_f16 a[0:15], v[0:3], v[4:7], a[0:15]",
+      "ds_read_b32 v8, v235"], 1),
+    (["buffer_store_dwordx4 v[6:9], v20, s[24:27], 0 offen nt", "v_add_u32_e32 v10, 1, v6", "v_mov_b32_e32 v11, 0",
+      "v_mov_b32_e32 v6, 0"], 0),                               # (reads, other registers, then 2 states passed)
+    (["buffer_store_dword v6, v20, s[24:27], 0 offen", "v_mov_b32_e32 v6, 0"], 0),   # 4-byte store: no hazard
+    (["global_store_dwordx4 v[0:1], v[6:9], off", "v_mov_b32_e32 v7, 0"], 1),
+])
+def test_store_data_rule(insns, n_bad):
+    assert len(check_isa.check_store_data(insns)) == n_bad, insns
+
+
+def test_store_data_overwrite_in_shipped_kernel_is_caught(disasm):
+    """The shipped training forward with a VALU write of a store's first data VGPR inserted right behind
+    it fails; with two wait states before that write it passes again."""
+    lines = disasm.splitlines()
+    inside = False
+    for i, ln in enumerate(lines):
+        if re.match(r"^[0-9a-f]+ <.*>:$", ln):
+            inside = "mlp16_kernel<true>" in ln
+        elif inside and "buffer_store_dwordx4" in ln:
+            first = re.search(r"buffer_store_dwordx4\s+v\[(\d+):", ln).group(1)
+            break
+    bad = lines[:i + 1] + [f"\tv_mov_b32_e32 v{first}, 0"] + lines[i + 1:]
+    report, _ = check_isa.check("\n".join(bad))
+    assert any("mlp16_kernel<true>" in n and any("wait state" in b for b in v) for n, v in report.items()), report
+    padded = lines[:i + 1] + ["\ts_nop 1", f"\tv_mov_b32_e32 v{first}, 0"] + lines[i + 1:]
+    report, _ = check_isa.check("\n".join(padded))
+    assert report == {}, report

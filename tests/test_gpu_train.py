@@ -2,8 +2,8 @@
 on the oracle (oracle/nerf_oracle.py, pinned to the reference by F7) — SURVEY.md §8f row 2.
 
 Every test runs under both MLP arithmetics: "f32" (fp32 MFMA throughout) and the default "f16x3"
-(split-f16 forward and data gradients, bf16x6 weight gradients: fp32-level results from
-multi-part products).  Against a float64 autograd of the same inputs, gradients
+(split-f16 forward, data gradients and weight gradients, with per-chunk block scales in the weight
+gradients: fp32-level results from multi-part products).  Against a float64 autograd of the same inputs, gradients
 agree to ~1e-5 relative in L2; a ReLU whose
 pre-activation sits within fp32 rounding of 0 can flip its mask between fp32 and fp64 and
 perturb single entries, so per-layer checks bound the relative L2 error (2e-4) and require
@@ -644,8 +644,8 @@ def test_param_grads_ray_path(ref_state, app_vec, app_kind, N):
     """nerf_param_grads with N >= 32 samples per ray: the per-ray gradient sums (dir_linear's PE_4(d)
     columns, the appearance projection and the appearance rows as GEMMs over rays), dir/sigma on the
     whole-tile GEMM, the two-stream schedule.  N = 40: tile-major blocks straddle rays (ray_sums_kernel);
-    N = 64 under f16x3: the fused sums (the dir/density launch's 8-sample sums of d pre_dir,
-    block_head_sums_kernel's d hd block sums).  Against the oracle's float64 autograd, and two calls
+    N = 64 under f16x3: the fused sums (the dir/density launch's 8-sample sums of d pre_dir, the rgb
+    head launch's d hd block sums, wgrad_head3_kernel<true>).  Against the oracle's float64 autograd, and two calls
     bit-identical (fixed-order reductions on both streams)."""
     L = _lib()
     lib, dev = L.load(), L.device()
