@@ -131,10 +131,17 @@ def test_validation_render_matches_volume_render(trained, tmp_path):
     rgb, depth = validation_render(model, ds, cfg, 7, str(tmp_path))
     assert os.path.exists(tmp_path / "render_000007.png")
     val = ds.get_rays(idx=len(ds) - 1)
-    r2, d2, _ = volume_render(model, val["rays_o"][:1000], val["rays_d"][:1000], 2.0, 6.0, cfg.num_samples, 0,
-                              appearance_embedding=ds.appearance_embeddings[len(ds) - 1], perturb=False)
+    args = (model, val["rays_o"][:1000], val["rays_d"][:1000], 2.0, 6.0, cfg.num_samples, 0)
+    kw = dict(appearance_embedding=ds.appearance_embeddings[len(ds) - 1], perturb=False)
+    with torch.no_grad():                              # (train.py:128-140 renders under no_grad)
+        r2, d2, _ = volume_render(*args, **kw)
     assert rgb.shape == (576, 3)                       # the first 1000 rays of a 24x24 image: all 576
     assert torch.equal(rgb, r2) and torch.equal(depth, d2)
+    # With gradients enabled the same call takes the differentiable path, whose forward is the
+    # training kernel (32 x 32 MFMA tiles; the render kernel runs 16 x 16 x 32): the same
+    # arithmetic with the products summed in another order inside the MFMA, so equal to fp32 rounding
+    r3, d3, _ = volume_render(*args, **kw)
+    assert torch.allclose(r3, r2, rtol=1e-5, atol=1e-6) and torch.allclose(d3, d2, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("arith", ["f16x3", "f32"])
