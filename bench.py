@@ -28,10 +28,11 @@ samples: 192 evaluations per ray).  achieved = algorithmic FLOP / kernel time, t
 live in the timed steps by HIP events the library records on the launch's own stream around each
 MLP launch inside nerf_render_rays (nerf_profile_mlp_begin/_end; no change to what runs).
 --arith selects the MLP arithmetic (include/nerfmi.h, nerf_arith), both fp32-accurate:
-  f16x3 (default, mlp16_kernel): every fp32 product is three f16 MFMA products of a hi/lo split;
+  f16x3 (default, mlp16s_kernel): every fp32 product is three f16 MFMA products of a hi/lo split;
         peak = the f16 dense MFMA peak / 3 = 2516.8 / 3 = 838.9 TFLOP/s of fp32-equivalent work
         (MI355X_MICROARCH.md: f16 = 16x the f32 MFMA rate); "mfma_busy" reports the issued f16
-        MFMA FLOP (3072 v_mfma_f32_32x32x16_f16 per 32 samples) against 2516.8 TFLOP/s;
+        MFMA FLOP (6144 v_mfma_f32_16x16x32_f16 per 32 samples, the FLOP of 3072 32x32x16) against
+        2516.8 TFLOP/s;
   f32   (mlp_kernel): v_mfma_f32_32x32x2_f32, peak 157.3 TFLOP/s.
 cpu_baseline: the oracle (PyTorch-CPU restatement, oracle/nerf_oracle.py) timed on a
 bounded sample of the same workload on this host's cores (rank 0, N=1 only); the GPU renders
@@ -70,7 +71,7 @@ N_COARSE, N_FINE = 64, 128
 FLOP_PER_SAMPLE = 1_048_832           # SURVEY.md §8d, DESIGN.md §Roofline
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
 MFMA_F16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # f16/bf16 dense MFMA = 16x the f32 rate
-F16X3_ISSUED_FLOP_PER_SAMPLE = 3072 * 32 * 32 * 16 * 2 // 32   # mlp16_kernel MFMAs per 32-sample wave
+F16X3_ISSUED_FLOP_PER_SAMPLE = 6144 * 16 * 16 * 32 * 2 // 32   # mlp16s_kernel MFMAs per 32-sample wave
 # Measured power-limited ceiling of the f16 MFMA stream mlp16 is built from: the
 # trunk half-step alone (12 v_mfma_f32_32x32x16_f16 + 8 LDS fragment reads, no side work, every CU,
 # random operands) holds 1.44 GHz = 1,447 f16 TFLOP/s = 482 TFLOP/s of f16x3 work.
@@ -269,7 +270,7 @@ def mlp_roofline(launches, arith):
     if arith == "f16x3":
         busy = mlp_samples * F16X3_ISSUED_FLOP_PER_SAMPLE / (mlp_ms * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS \
             if mlp_ms else 0.0
-        return achieved, MFMA_F16_PEAK_TFLOPS / 3, "nerf::mlp16_kernel", busy
+        return achieved, MFMA_F16_PEAK_TFLOPS / 3, "nerf::mlp16s_kernel", busy
     return achieved, MFMA_F32_PEAK_TFLOPS, "nerf::mlp_kernel", achieved / MFMA_F32_PEAK_TFLOPS
 
 
