@@ -27,6 +27,7 @@ def main():
     cfg = nerfmi.Config()
     torch.manual_seed(0)
     tr = Trainer(cfg)
+    L.check(lib.nerf_pack_weights(tr.param_ptrs, P(tr.packed), s), "pack")   # (a Trainer packs in its step)
     B, N = 4096, cfg.num_samples
     M = B * N
     g = torch.Generator().manual_seed(1)

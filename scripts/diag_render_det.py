@@ -22,6 +22,7 @@ def main():
     dev = L.device()
     torch.manual_seed(0)
     tr = Trainer(nerfmi.Config())
+    L.check(lib.nerf_pack_weights(tr.param_ptrs, P(tr.packed), s), "pack")   # (a Trainer packs in its step)
     g = torch.Generator().manual_seed(1)
     app = torch.randn(1, 32, generator=g).to(dev)
     for R, N in ((576, 32), (576, 64), (1000, 32), (4096, 64), (777, 48)):
