@@ -91,7 +91,12 @@ __device__ __forceinline__ void smfma_tile(const STile& a, const Operand& b0, co
 
 // One tile segment: side work phase 0 (its LDS reads first), the fragment reads (NRD tiles' worth,
 // `reads`), tile TI's MFMAs (+ hook), side phase 1, interleaved: per MFMA gap one MFMA, one DS read
-// (gaps 1..4 per tile read), VPG VALU.
+// (gaps 1..4 per tile read), VPG VALU from gap kSValuGap0 on.  The side's VALU waits for its LDS reads
+// (biases, density weights), issued at the segment's start; a 16x16x32 MFMA issues in half the cycles
+// of a 32x32x16 one, so mlp16's gap 1 left them ~2 MFMAs of cover and the in-order wave stalled
+// there with the MFMA pipe drained.  From gap 5 (7 gaps of VALU): +2.2-2.9 % frame rate, same box
+// (gap 3 +1.9 %, 7 the same as 5, 9 +1.2-2.5 %; profiles/r06/ab_render_vgap*.log).
+constexpr int kSValuGap0 = 5;
 template <int G, int TI, bool FIRST, int NRD, int VPG, typename Reads, typename Side, typename Hook>
 __device__ __forceinline__ void ssegment(const STile& a, const Operand& b0, const Operand& b1, SAcc& acc, Reads&& reads,
                                          Side&& side, Hook&& hook) {
@@ -104,7 +109,7 @@ __device__ __forceinline__ void ssegment(const STile& a, const Operand& b0, cons
   for (int i = 0; i < 12; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                        // 1 MFMA
     if (i >= 1 && i <= 4 * NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-    if (VPG > 0 && i >= 1) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VALU
+    if (VPG > 0 && i >= kSValuGap0) __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);   // VALU
   }
   __builtin_amdgcn_sched_barrier(0);
 }
@@ -148,7 +153,7 @@ __device__ __forceinline__ constexpr int side_count(int i, int seg) {
 template <int KIND>
 __device__ __forceinline__ constexpr int svpg(int i, int seg) {
   const int n = side_count<KIND>(i, seg);
-  return n == 0 ? 0 : (n * 40 + 10) / 11;
+  return n == 0 ? 0 : (n * 40 + 11 - kSValuGap0) / (12 - kSValuGap0);   // ~40 VALU per quarter
 }
 
 // One chunk-step: chunk c (global index, ring slot SLOT) = k-step i of group G; b0 / b1 its sample
