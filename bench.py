@@ -72,11 +72,15 @@ FLOP_PER_SAMPLE = 1_048_832           # SURVEY.md §8d, DESIGN.md §Roofline
 MFMA_F32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
 MFMA_F16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # f16/bf16 dense MFMA = 16x the f32 rate
 F16X3_ISSUED_FLOP_PER_SAMPLE = 6144 * 16 * 16 * 32 * 2 // 32   # mlp16s_kernel MFMAs per 32-sample wave
-# Measured power-limited ceiling of the f16 MFMA stream mlp16 is built from: the
-# trunk half-step alone (12 v_mfma_f32_32x32x16_f16 + 8 LDS fragment reads, no side work, every CU,
-# random operands) holds 1.44 GHz = 1,447 f16 TFLOP/s = 482 TFLOP/s of f16x3 work.
-F16X3_POWER_CEILING = {"value": 1447.0 / 3, "unit": "TFLOP/s",
-                       "source": "profiles/r02_mfma_shape_side.log (scripts/microbench/mfma_shape_side.hip, NV=0)"}
+# Measured power-limited ceiling of the f16 MFMA stream the render kernel is built from:
+# the trunk's MFMAs alone with their LDS fragment reads, no side work, every CU, random operands.  The
+# render kernel runs v_mfma_f32_16x16x32_f16 since round 6: that stream holds 1.99 GHz = 1,574 f16
+# TFLOP/s = 525 TFLOP/s of f16x3 work; the 32x32x16 stream of round 5's kernel (and of the training
+# kernels) 1.44 GHz = 1,447 f16 TFLOP/s = 482 TFLOP/s.
+F16X3_POWER_CEILING = {"value": 1574.0 / 3, "unit": "TFLOP/s", "shape": "v_mfma_f32_16x16x32_f16",
+                       "source": "profiles/r02_mfma_shape_side.log (scripts/microbench/mfma_shape_side.hip, "
+                                 "shape 16, NV=0)",
+                       "shape_32x32x16": {"value": 1447.0 / 3, "unit": "TFLOP/s"}}
 # The vendor library's sustained f16 GEMM on the same part (torch.matmul -> hipBLASLt, 8192^3, random
 # operands, 3 s back to back): 1,323.5 TFLOP/s = 0.526 of the dense f16 peak.
 VENDOR_F16_GEMM = {"f16_tflops": 1323.5, "frac_of_f16_peak": 1323.5 / MFMA_F16_PEAK_TFLOPS,
