@@ -638,15 +638,16 @@ def _oracle_grads_f32(state, app, R, N, draw):
     return {k: v.grad.numpy() for k, v in sd.items() if v.grad is not None}
 
 
-@pytest.mark.parametrize("N", [40, 64])
+@pytest.mark.parametrize("N", [32, 40, 64])
 @pytest.mark.parametrize("app_kind", ["broadcast", "per_ray", "none"])
 def test_param_grads_ray_path(ref_state, app_vec, app_kind, N):
     """nerf_param_grads with N >= 32 samples per ray: the per-ray gradient sums (dir_linear's PE_4(d)
     columns, the appearance projection and the appearance rows as GEMMs over rays), dir/sigma on the
     whole-tile GEMM, the two-stream schedule.  N = 40: tile-major blocks straddle rays (ray_sums_kernel);
-    N = 64 under f16x3: the fused sums (the dir/density launch's 8-sample sums of d pre_dir, the rgb
-    head launch's d hd block sums, wgrad_head3_kernel<true>).  Against the oracle's float64 autograd, and two calls
-    bit-identical (fixed-order reductions on both streams)."""
+    N = 32 and 64 under f16x3: the fused sums (the dir/density launch's 8-sample sums of d pre_dir, the
+    rgb head launch's d hd block sums, wgrad_head3_kernel<true>; N = 32: one ray per 32-sample block).
+    Against the oracle's float64 autograd, and two calls bit-identical (fixed-order reductions on both
+    streams)."""
     L = _lib()
     lib, dev = L.load(), L.device()
     R = 48
