@@ -1,7 +1,7 @@
 # Round 6 evidence at HEAD: the whole GPU suite (both arithmetics) and smoke.
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r06/k2
+O=gpurun_out/r06/kf
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread \
   > $O/pytest_gpu.log 2>&1

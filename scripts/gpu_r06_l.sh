@@ -2,7 +2,7 @@
 # bench_train.py, and the PMC traffic passes (render f16x3, training).
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r06/l3
+O=gpurun_out/r06/lf
 mkdir -p $O
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 600 $O/bench.log; echo
