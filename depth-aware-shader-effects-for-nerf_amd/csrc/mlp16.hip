@@ -1,5 +1,9 @@
-// Fused positional encoding -> NeRF MLP forward on split-f16 MFMA ("f16x3"), the render
-// path's default MLP arithmetic (R4-R6; reference src/models.py:105-162, :14-47).
+// Fused positional encoding -> NeRF MLP forward on split-f16 MFMA ("f16x3") with the training saves
+// (R4-R6 + §8f-2; reference src/models.py:105-162, :14-47): the forward of nerf_mlp_forward_train /
+// nerf_train_forward.  Since round 6 the render calls run mlp16s_kernel (mlp16s.hip: the same
+// arithmetic and weight stream on v_mfma_f32_16x16x32_f16), so this kernel is instantiated with
+// SAVE = true only; its SAVE = false branches (the round-5 render kernel) are not compiled into the
+// library, and the DESIGN §4 measurements of that kernel come from the round-5 sources (git history).
 //
 // Arithmetic.  Every dense layer out^T = W . in^T runs on v_mfma_f32_32x32x16_f16 as
 //     hi(W) hi(a) + hi(W) lo(a) + lo(W) hi(a)       (f32 accumulation)
