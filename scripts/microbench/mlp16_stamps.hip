@@ -1,11 +1,11 @@
 // Diagnostic: per-wave segment durations (s_memtime) of mlp16_kernel (the f16x3 MLP) on the
-// (Round 6: launch_mlp16 without saves runs mlp16s_kernel, which has no stamps; this tool timed the
-// round-5 render kernel and needs round 5's csrc/mlp16.hip, e.g. from `git show 5134bc2:...`.)
 // coarse pass of an 800x800 frame (640,000 rays x 64 samples), synthetic inputs.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DNERF_MLP16_STAMPS \
 //     -I depth-aware-shader-effects-for-nerf_amd/csrc -o scripts/microbench/mlp16_stamps scripts/microbench/mlp16_stamps.hip
 // Stamps: 0 start | 1 prologue done (PE, first chunk) | 2 + L after trunk layer L (0..7; each
 // layer's epilogue runs inside the next layer's MFMAs) | 10 after the colour layer | 11 end.
+// (Round 6: launch_mlp16 without saves runs mlp16s_kernel, which has no stamps; this tool timed the
+// round-5 render kernel and needs round 5's csrc/mlp16.hip, e.g. from `git show 5134bc2:...`.)
 #include "../../depth-aware-shader-effects-for-nerf_amd/csrc/mlp16.hip"
 #include <algorithm>
 #include <stdarg.h>
