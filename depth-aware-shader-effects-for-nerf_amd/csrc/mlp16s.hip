@@ -95,7 +95,7 @@ __device__ __forceinline__ void smfma_tile(const STile& a, const Operand& b0, co
 // (biases, density weights), issued at the segment's start; a 16x16x32 MFMA issues in half the cycles
 // of a 32x32x16 one, so mlp16's gap 1 left them ~2 MFMAs of cover and the in-order wave stalled
 // there with the MFMA pipe drained.  From gap 5 (7 gaps of VALU): +2.2-2.9 % frame rate, same box
-// (gap 3 +1.9 %, 7 the same as 5, 9 +1.2-2.5 %; profiles/r06/ab_render_vgap*.log).
+// (gap 3 +1.9 %, 4 and 6 within 0.2 % of 5, 7 the same, 9 +1.2-2.5 %; profiles/r06/ab_render_vgap*.log).
 constexpr int kSValuGap0 = 5;
 template <int G, int TI, bool FIRST, int NRD, int VPG, typename Reads, typename Side, typename Hook>
 __device__ __forceinline__ void ssegment(const STile& a, const Operand& b0, const Operand& b1, SAcc& acc, Reads&& reads,
