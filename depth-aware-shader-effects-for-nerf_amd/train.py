@@ -114,7 +114,6 @@ class Trainer:
         self._ws = None
         self._tvals = {}
         self._side = None          # side stream for the transposed packing (forward_backward)
-        self._side_on = os.environ.get("NERFMI_PACKT_SIDE", "1") != "0"   # (0: same-box A/B)
 
     def view(self, buf, i):
         return buf[self.offsets[i]: self.offsets[i + 1]].view(self.shapes[i])
@@ -147,7 +146,7 @@ class Trainer:
         # backward read them; joined before this step's backward).
         main = torch.cuda.current_stream(self.dev)
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.dev) if self._side_on else main
+            self._side = torch.cuda.Stream(device=self.dev)
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self._fork.record(main)
         self._side.wait_event(self._fork)
